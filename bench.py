@@ -1,0 +1,254 @@
+#!/usr/bin/env python3
+"""Headline benchmark: brute-force cosine kNN on 1M x 512 per GPU, top-k = 10.
+
+Metric (BASELINE.json): "CLIP img-embeds/sec/GPU; kNN queries/sec on 1M×512 at
+top-k=10, 1/2/4/8 GPUs". ``value`` is the kNN leg: whole-job queries/s, where one
+query = one 512-d query scanned against one GPU's 1M-row shard (BASELINE config 3
+at N=1; config 4's row-sharded layout at N>1: rank r holds global rows
+[r*2^20, (r+1)*2^20), every step answers the same 1000 queries against all N*2^20
+rows and ends with an RCCL all-gather of the per-shard top-k + the K11 merge).
+Weak scaling: per-GPU work is fixed as N grows; value = N * 1000 * steps / t.
+
+A step = one ``FlatIndex.search`` of 1000 queries (inputs already in HBM): query
+prep, K7 fp16 MFMA scan, K8 merge + exact f64 rescore + certificate, the
+(normally empty) collect pass, and for N>1 the all-gather + merge. The CLIP
+ViT-B/32 leg (config 2) is reported beside it as ``clip`` when the encoder
+library is present.
+
+Run: python bench.py [--gpus N --steps K --warmup W]; N>1 under
+torch.distributed.run (one process per GPU, RCCL).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "multimodal-rag-for-image-text-search_amd")
+for p in (PKG, ROOT):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+ROWS_PER_GPU = 1 << 20
+DIM = 512
+NQ = 1000
+TOPK = 10
+MFMA_FP16_PEAK_TFLOPS = 2500.0  # dense fp16/bf16 MFMA, MI355X_MICROARCH.md
+HBM_PEAK_GBS = 8000.0
+
+
+def _dist_setup():
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return world, rank, local
+
+
+def _max_over_ranks(x: float, world: int) -> float:
+    if world == 1:
+        return x
+    import torch
+    import torch.distributed as dist
+
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def _barrier(world: int):
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.barrier()
+
+
+def cpu_baseline(seconds_budget: float = 20.0):
+    """The oracle (exact f64 numpy flat cosine, oracle/knn.py) on the host cores, on a
+    bounded sample of the same workload: 1M x 512 corpus, as many of the 1000
+    queries as fit ~budget seconds (at least 8)."""
+    import numpy as np
+
+    from oracle.knn import flat_cosine_topk
+
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except Exception:
+        cores = os.cpu_count() or 1
+    try:
+        from threadpoolctl import threadpool_info
+
+        blas_threads = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
+    except Exception:
+        blas_threads = cores
+    rng = np.random.default_rng(0)
+    x = rng.standard_normal((ROWS_PER_GPU, DIM), dtype=np.float32)
+    x /= np.linalg.norm(x, axis=1, keepdims=True)
+    q = rng.standard_normal((NQ, DIM), dtype=np.float32)
+    lab = np.zeros(ROWS_PER_GPU, dtype=np.int32)
+    t0 = time.perf_counter()
+    flat_cosine_topk(x, lab, q[:8], TOPK)
+    t8 = time.perf_counter() - t0
+    nq = int(min(NQ, max(8, 8 * seconds_budget / max(t8, 1e-6))))
+    nq = max(8, (nq // 8) * 8)
+    if nq > 8:
+        t0 = time.perf_counter()
+        flat_cosine_topk(x, lab, q[:nq], TOPK)
+        dt = time.perf_counter() - t0
+    else:
+        dt = t8
+    return {
+        "value": round(nq / dt, 3),
+        "unit": "queries/s (1M x 512 shard, top-10)",
+        "cores": int(min(cores, blas_threads)),
+        "kind": "port",
+        "sample": f"oracle.knn.flat_cosine_topk (exact f64 numpy) on {nq} of the 1000 queries "
+                  f"against the same 1M x 512 corpus shape, {dt:.1f} s",
+    }
+
+
+def _traffic_from_profiles():
+    """HBM bytes per K7 launch from the committed rocprofv3 PMC pass (or None)."""
+    path = os.path.join(ROOT, "profiles", "knn_scan_pmc.json")
+    try:
+        with open(path) as f:
+            return float(json.load(f)["hbm_bytes_per_launch"])
+    except Exception:
+        return None
+
+
+def clip_leg(steps: int, warmup: int):
+    """CLIP ViT-B/32 image embeds/s on one GPU (config 2: batch 256, fp16)."""
+    try:
+        from app.encoders import bench_clip_images
+    except Exception:
+        return None
+    return bench_clip_images(steps=steps, warmup=warmup)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-clip", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world, rank, local = _dist_setup()
+    if world != args.gpus:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    dev = torch.device("cuda", local)
+
+    from app.vector_store import FlatIndex, topk_merge
+
+    # shard r of the 8M x 512 corpus (config 4): seed (0, r), generated on device
+    g = torch.Generator(device=dev).manual_seed(1000 + rank)
+    x = torch.randn((ROWS_PER_GPU, DIM), generator=g, device=dev)
+    x = x / x.norm(dim=1, keepdim=True)
+    index = FlatIndex(DIM, device=local)
+    index.add(x)
+    del x
+    torch.cuda.empty_cache()
+    gq = torch.Generator(device=dev).manual_seed(1)
+    q = torch.randn((NQ, DIM), generator=gq, device=dev)  # same queries on every rank
+    row_offset = rank * ROWS_PER_GPU
+
+    gath_s = gath_r = None
+    if world > 1:
+        gath_s = torch.empty((world, NQ, TOPK), dtype=torch.float64, device=dev)
+        gath_r = torch.empty((world, NQ, TOPK), dtype=torch.int64, device=dev)
+
+    def step():
+        s, r, s64 = index.search(q, TOPK, row_offset=row_offset, with_f64=True)
+        if world > 1:
+            dist.all_gather_into_tensor(gath_s, s64)
+            dist.all_gather_into_tensor(gath_r, r)
+            s, r, _ = topk_merge(gath_s, gath_r, TOPK)
+        return s, r
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    index.profile(1)
+    _barrier(world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    _barrier(world)
+    dt = time.perf_counter() - t0
+    scan_ms, scan_n = index.profile(0)
+    unc, _ = index.last_stats()
+    dt = _max_over_ranks(dt, world)
+
+    ms_per_step = dt / args.steps * 1e3
+    value = world * NQ * args.steps / dt
+    avg_scan_s = (scan_ms / max(scan_n, 1)) / 1e3
+    flops_per_launch = 2.0 * NQ * ROWS_PER_GPU * DIM
+    achieved_tflops = flops_per_launch / avg_scan_s / 1e12 if avg_scan_s > 0 else 0.0
+
+    if rank == 0:
+        out = {
+            "metric": "CLIP img-embeds/sec/GPU; kNN queries/sec on 1M×512 at top-k=10, 1/2/4/8 GPUs",
+            "value": round(value, 3),
+            "unit": "queries/s (1000-query batches, each query scanned against a 1M x 512 shard per GPU, top-10; aggregate over GPUs)",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp16 MFMA scan + f64 exact rescore",
+            "data": "synthetic (N(0,1) rows L2-normalised, seeded; queries N(0,1))",
+            "config": {
+                "workload": "BASELINE config 3 (N=1) / config 4 (N>1): brute-force cosine top-10, 1M x 512 rows per GPU, 1000-query batch",
+                "rows_per_gpu": ROWS_PER_GPU,
+                "total_rows": ROWS_PER_GPU * world,
+                "dim": DIM,
+                "queries_per_step": NQ,
+                "top_k": TOPK,
+                "parallelism": f"row-sharded x{world}" + (" + RCCL all-gather of per-shard top-k" if world > 1 else ""),
+                "query_vector_pairs_per_s": round(value * ROWS_PER_GPU, 1),
+                "uncertified_queries_last_step": unc,
+            },
+            "roofline": {
+                "kernel": "knn_scan_kernel<512,16> (K7)",
+                "bound": "mfma",
+                "achieved": round(achieved_tflops, 2),
+                "peak": MFMA_FP16_PEAK_TFLOPS,
+                "unit": "TFLOP/s",
+                "frac": round(achieved_tflops / MFMA_FP16_PEAK_TFLOPS, 4),
+                "traffic": _traffic_from_profiles(),
+                "avg_launch_ms": round(avg_scan_s * 1e3, 4),
+                "algorithmic_flops_per_launch": flops_per_launch,
+                "algorithmic_bytes_per_launch": ROWS_PER_GPU * DIM * 2 + NQ * DIM * 2,
+            },
+        }
+        if not args.no_clip:
+            clip = clip_leg(steps=max(5, args.steps // 2), warmup=2)
+            if clip is not None:
+                out["clip"] = clip
+        if not args.no_cpu_baseline and world == 1:
+            out["cpu_baseline"] = cpu_baseline()
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

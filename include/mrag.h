@@ -1,0 +1,126 @@
+/*
+ * mrag.h — C ABI of the MI355X embed-and-retrieve engine (libmrag.so, gfx950).
+ *
+ * This is the drop-in boundary for the reference's hot path. The reference
+ * (Sabarna07-tech/Multimodal-RAG-for-Image-Text-Search) is pure Python; its
+ * numerics sit behind two FFI-like seams that this library replaces:
+ *
+ *   - lancedb (Rust) flat cosine scan + top-k, reached from
+ *       app/storage/lancedb_store.py:103-123  (search_text / search_image)
+ *       app/storage/lancedb_store.py:87-101   (upsert_text_vectors / upsert_image_vectors)
+ *       app/storage/lancedb_store.py:63-69    (LanceDBStore._normalize)
+ *   - torch/transformers encoder forwards, reached from
+ *       app/ml/embeddings.py:46-49            (_normalize)
+ *       app/ml/embeddings.py:62-70            (SentenceTransformer.encode, MiniLM-L6)
+ *       app/ml/embeddings.py:84-91            (CLIP get_image_features, ViT-B/32)
+ *       app/ml/embeddings.py:101-105          (CLIP get_text_features)
+ *
+ * Conventions:
+ *   - every entry point returns int status, 0 == MRAG_OK; on failure the
+ *     thread-local message is available from mrag_last_error();
+ *   - plain pointers and sizes only; `ptr_kind` says whether data pointers are
+ *     host (MRAG_PTR_HOST) or device (MRAG_PTR_DEVICE) memory;
+ *   - `stream` is a hipStream_t passed as void* (NULL = the handle's stream);
+ *   - handles are opaque; calls on one handle are serialised by an internal
+ *     mutex, so a handle may be used from any single thread at a time.
+ */
+#ifndef MRAG_H
+#define MRAG_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ------------------------------------------------------ */
+#define MRAG_OK 0
+#define MRAG_ERR_ARG 1         /* bad argument (shape, pointer, k, dim, ...)      */
+#define MRAG_ERR_HIP 2         /* a HIP runtime call failed                       */
+#define MRAG_ERR_OOM 3         /* device allocation failed                        */
+#define MRAG_ERR_STATE 4       /* handle in the wrong state                       */
+#define MRAG_ERR_UNSUPPORTED 5 /* no kernel instance for this configuration       */
+
+#define MRAG_PTR_HOST 0
+#define MRAG_PTR_DEVICE 1
+
+/* Row labels: the reference filters every search with `user_id == '<id>'`
+ * (lancedb_store.py:108,119). The engine stores one int32 label per row (the
+ * host maps user ids to labels). Label filter MRAG_LABEL_ANY matches every
+ * live row; rows whose label is MRAG_LABEL_DELETED are tombstones (upsert's
+ * per-row delete, lancedb_store.py:91-92) and never match. */
+#define MRAG_LABEL_ANY (-1)
+#define MRAG_LABEL_DELETED (-2)
+
+const char* mrag_last_error(void);
+const char* mrag_version(void);
+int mrag_get_device_count(int32_t* count);
+
+/* ---- K6: row L2-normalise ---------------------------------------------
+ * Replaces app/ml/embeddings.py:46-49 `_normalize`:
+ *   y[r,:] = x[r,:] / ||x[r,:]||  (zero rows copied unchanged)
+ * computed in f32 with numpy's pairwise summation order for the row sum of
+ * squares, so the result is bit-identical to the reference's numpy call.
+ * x, y: device pointers [rows, dim] row-major f32 (y may alias x). */
+int mrag_l2norm_rows(const float* x, float* y, int64_t rows, int32_t dim, void* stream);
+
+/* ---- K7/K8: flat cosine index ------------------------------------------
+ * Replaces the Lance table + `table.search(v).where(user_id).metric("cosine")
+ * .limit(max(k,1))` chain (lancedb_store.py:103-123). One index = one table
+ * (text_collection or image_collection, lancedb_store.py:30-31) or one shard
+ * of it. Exact semantics: score = cos(q, x) = q.x / (|q| |x|) evaluated in
+ * f64 on the f32 vectors as given (0 if either norm is 0), results ordered by
+ * (score desc, row asc), label prefilter, at most k rows. */
+typedef struct mrag_knn_index mrag_knn_index;
+
+int mrag_knn_create(int32_t dim, int32_t device, mrag_knn_index** out);
+int mrag_knn_destroy(mrag_knn_index* index);
+
+/* Append n rows (f32 [n, dim]) with their labels (int32 [n]); the new rows get
+ * consecutive row ids starting at *first_row (the current size). */
+int mrag_knn_add(mrag_knn_index* index, const float* rows, const int32_t* labels, int64_t n,
+                 int32_t ptr_kind, int64_t* first_row);
+
+/* Overwrite the label of rows[i] (host int64 [n]); MRAG_LABEL_DELETED deletes. */
+int mrag_knn_set_labels(mrag_knn_index* index, const int64_t* rows, int64_t n, int32_t label);
+
+/* Number of row ids handed out so far (live + deleted). */
+int mrag_knn_size(const mrag_knn_index* index, int64_t* n);
+
+/* Search nq queries (f32 [nq, dim]) for their k best rows among rows whose
+ * label matches `label_filter`. out_scores f32 [nq, k], out_rows int64
+ * [nq, k]; row ids are offset by `row_offset` (a shard's first global row).
+ * Slots past the number of matching rows get score -inf and row -1.
+ * out_scores64 (optional, may be NULL) receives the f64 scores used for the
+ * ordering — the sharded merge needs them. All data pointers share ptr_kind. */
+int mrag_knn_search(mrag_knn_index* index, const float* queries, int64_t nq, int32_t k,
+                    int32_t label_filter, int64_t row_offset, float* out_scores,
+                    double* out_scores64, int64_t* out_rows, int32_t ptr_kind, void* stream);
+
+/* Statistics of the last search on this handle: number of queries whose fp16
+ * candidate pass could not be certified exact and went through the
+ * threshold-collect pass, and how many collect retries overflowed. */
+int mrag_knn_last_stats(const mrag_knn_index* index, int64_t* uncertified, int64_t* retries);
+
+/* Kernel timing for roofline reporting: HIP events recorded on the search
+ * stream around every K7 scan launch. enable = 1 resets and enables, 0
+ * disables, -1 only reads. Outputs (optional): total scan milliseconds and the
+ * number of timed launches since the last reset. */
+int mrag_knn_profile(mrag_knn_index* index, int32_t enable, double* scan_ms_total,
+                     int64_t* scan_launches);
+
+/* ---- K11: merge per-shard top-k lists (row-sharded multi-GPU search) ----
+ * Input: nlists lists per query laid out [nlists][nq][k] (f64 score, int64
+ * global row; row -1 = empty), e.g. the result of an RCCL all-gather of every
+ * rank's mrag_knn_search output. Output: the k best per query under
+ * (score desc, row asc) — identical to a single-index search.
+ * Device pointers. */
+int mrag_topk_merge(const double* scores64, const int64_t* rows, int32_t nlists, int64_t nq,
+                    int32_t k, float* out_scores, double* out_scores64, int64_t* out_rows,
+                    void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MRAG_H */

@@ -1,0 +1,1066 @@
+// knn.hip — K7/K8/K10/K11: exact flat cosine top-k over a device-resident corpus.
+//
+// Replaces the lancedb flat cosine scan behind app/storage/lancedb_store.py:103-123
+// (`table.search(v).where("user_id == ...").metric("cosine").limit(max(k,1))`) and
+// the per-row upsert at :87-101. Semantics are pinned in DESIGN.md §3:
+//   score(q, x) = q.x / (|q| |x|) in f64 on the f32 vectors as given (0 on a zero
+//   norm), label prefilter, order (score desc, row asc), at most k rows.
+//
+// Pipeline per search (all on one HIP stream):
+//   prep   : queries f32 -> q32 (padded), |q| (f64), q16 = fp16(q/|q|)
+//   K7 scan: MFMA fp16 Q.Dt over the fp16 scan copy of the corpus; every lane keeps
+//            a running top-KL of the rows it sees; one list per (query, split)
+//   K8     : per query, union of the split lists -> M best by approximate score ->
+//            exact f64 rescoring against the f32 master rows -> certificate:
+//            every row outside the candidate set has approx <= T, approx is within
+//            EPS of exact, so if exact_k > T + EPS the top-k is proven exact
+//   K7c    : (only for uncertified queries) threshold-collect scan: every row with
+//            approx >= exact_k - EPS is collected — a superset of the true top-k
+//   K10    : exact f64 rescoring of the collected rows + ordered selection
+// The result is therefore exact for any data (ties and duplicates included), and
+// the common case costs one fp16 MFMA pass plus a small gather.
+//
+// HBM layout per index (rows padded to DP = dim rounded up to 128):
+//   x16    [cap][DP] fp16   normalised scan copy   (streamed by K7, 1 KiB rows at 512-d)
+//   x32    [cap][DP] f32    master rows as given   (gathered by K8/K10 only)
+//   xn     [cap]     f64    |x|
+//   labels [cap]     int32  user label, MRAG_LABEL_DELETED for tombstones / padding
+#include <algorithm>
+#include <mutex>
+#include <vector>
+
+#include "common.h"
+
+#define AS1 __attribute__((address_space(1)))
+#define AS3 __attribute__((address_space(3)))
+
+namespace {
+
+constexpr int TILE_ROWS = 64;
+constexpr int SCAN_WAVES = 8;
+constexpr int SCAN_THREADS = SCAN_WAVES * 64;
+constexpr int QPW = 32;                     // queries per wave (MFMA 32x32 N dim)
+constexpr int QPG = SCAN_WAVES * QPW;       // queries per workgroup
+constexpr int MAX_MERGE_ENTRIES = 4096;     // splits * KL cap (LDS sort in K8)
+constexpr int MAX_K = 256;
+constexpr int MERGE_THREADS = 256;
+
+// |approx - exact| bound for the fp16 scan:
+//   fp16 rounding of both unit vectors: (2u + u^2) * sum|q_i x_i| <= 9.77e-4 (u = 2^-11)
+//   f32 accumulation over <= 512 terms :  512 * 2^-24          <= 3.05e-5
+//   fp16 subnormal flush, f32 normalise:                        <= 4e-6
+constexpr double EPS_F16 = 1.05e-3;
+
+struct ScanParams {
+  const _Float16* x16;
+  const int32_t* labels;
+  const _Float16* q16;
+  int ntiles, qgroups, splits, Qp, label_filter;
+  // top-k mode
+  float* part_s;
+  int32_t* part_i;
+  // collect mode
+  const int32_t* fail_list;
+  const int32_t* fail_cnt;
+  const float* thresh;
+  int32_t* cand_cnt;
+  int32_t* cand;
+  int ccap;
+};
+
+template <int KL>
+__device__ __forceinline__ void list_insert(float (&ls)[KL], int (&li)[KL], float s, int r) {
+  float cs = s;
+  int cr = r;
+#pragma unroll
+  for (int j = 0; j < KL; ++j) {
+    const bool sw = cs > ls[j];
+    const float ts = ls[j];
+    const int tr = li[j];
+    ls[j] = sw ? cs : ts;
+    li[j] = sw ? cr : tr;
+    cs = sw ? ts : cs;
+    cr = sw ? tr : cr;
+  }
+}
+
+// K7 / K7c. One workgroup = 8 waves = 256 queries x one split of the corpus tiles
+// (tiles split, split+S, split+2S, ...). Corpus tiles (64 rows) are double-buffered in
+// LDS by global_load_lds (16 B/lane, rows XOR-swizzled on the source address so the
+// A-fragment ds_read_b128 is conflict-free); each wave keeps its 32 queries' B
+// fragments (all of DP) in VGPRs for the whole launch.
+template <int DP, int KL, bool COLLECT>
+__global__ __launch_bounds__(SCAN_THREADS) void knn_scan_kernel(ScanParams p) {
+  constexpr int KSTEPS = DP / 16;
+  constexpr int ROW_BYTES = DP * 2;
+  constexpr int TILE_BYTES = TILE_ROWS * ROW_BYTES;
+  constexpr int CPR = DP / 8;  // 16-byte chunks per row
+  constexpr int GLDS_PER_WAVE = TILE_BYTES / 1024 / SCAN_WAVES;
+  static_assert(TILE_BYTES % (1024 * SCAN_WAVES) == 0, "tile must split into 1 KiB pieces");
+  static_assert(CPR % 16 == 0, "swizzle needs rows of a multiple of 16 chunks");
+  constexpr int LBL_OFF = 2 * TILE_BYTES;
+  __shared__ __attribute__((aligned(16))) char smem[2 * TILE_BYTES + 2 * TILE_ROWS * 4];
+
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int h = lane >> 5;
+  const int r32 = lane & 31;
+
+  // block -> (query group, split). Blocks b, b+8, b+16, ... share an XCD (observed
+  // round-robin dispatch; speed only): the query groups of one split are placed in
+  // that stride so a corpus tile is fetched from HBM once per XCD and hits L2 after.
+  int qg, split;
+  {
+    const int b = blockIdx.x;
+    if ((p.splits & 7) == 0) {
+      const int xcd = b & 7, slot = b >> 3;
+      qg = slot % p.qgroups;
+      split = (slot / p.qgroups) * 8 + xcd;
+    } else {
+      qg = b % p.qgroups;
+      split = b / p.qgroups;
+    }
+  }
+
+  int nslots = p.Qp;
+  if constexpr (COLLECT) {
+    nslots = *p.fail_cnt;
+    if (qg * QPG >= nslots) return;  // uniform: no uncertified queries in this group
+  }
+  const int slot = qg * QPG + w * QPW + r32;  // query slot of this lane
+  const bool wave_active = (qg * QPG + w * QPW) < nslots;
+  const bool lane_active = slot < nslots;
+  int qrow = slot;
+  if constexpr (COLLECT) qrow = lane_active ? p.fail_list[slot] : 0;
+
+  half8 qf[KSTEPS];
+  if (wave_active) {
+    const _Float16* qr = p.q16 + (size_t)(lane_active ? qrow : 0) * DP + h * 8;
+#pragma unroll
+    for (int kk = 0; kk < KSTEPS; ++kk) qf[kk] = *(const half8*)(qr + kk * 16);
+  }
+  float thr = INFINITY;
+  if constexpr (COLLECT) {
+    if (lane_active) thr = p.thresh[qrow];
+  }
+
+  float ls[KL];
+  int li[KL];
+#pragma unroll
+  for (int j = 0; j < KL; ++j) {
+    ls[j] = -INFINITY;
+    li[j] = -1;
+  }
+
+  const int my_tiles = (split < p.ntiles) ? (p.ntiles - 1 - split) / p.splits + 1 : 0;
+
+  // per-lane LDS offsets of the 8 distinct (kk mod 8) A-fragment chunks
+  int offA[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) offA[j] = r32 * ROW_BYTES + (((2 * j + h) ^ (r32 & 15)) * 16);
+
+  auto stage = [&](int buf, int tile) {
+    const char* gt = (const char*)p.x16 + (size_t)tile * TILE_BYTES;
+    char* lt = smem + buf * TILE_BYTES;
+#pragma unroll
+    for (int i = 0; i < GLDS_PER_WAVE; ++i) {
+      const int piece = w * GLDS_PER_WAVE + i;
+      const int P = piece * 64 + lane;
+      const int row = P / CPR;
+      const int pos = P - row * CPR;
+      const int c = pos ^ (row & 15);
+      __builtin_amdgcn_global_load_lds((const AS1 void*)(gt + row * ROW_BYTES + c * 16),
+                                       (AS3 void*)(lt + piece * 1024), 16, 0, 0);
+    }
+    if (w == 0) {
+      __builtin_amdgcn_global_load_lds((const AS1 void*)(p.labels + (size_t)tile * TILE_ROWS + lane),
+                                       (AS3 void*)(smem + LBL_OFF + buf * TILE_ROWS * 4), 4, 0, 0);
+    }
+  };
+
+  auto epilogue = [&](const f32x16& acc, int cur, int rb, int tile) {
+    const int* lbl = (const int*)(smem + LBL_OFF + cur * TILE_ROWS * 4);
+    int4 L[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) L[g] = *(const int4*)(lbl + rb + 8 * g + 4 * h);
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      const int g = reg >> 2, e = reg & 3;
+      const int lab = e == 0 ? L[g].x : e == 1 ? L[g].y : e == 2 ? L[g].z : L[g].w;
+      const bool ok = (p.label_filter == MRAG_LABEL_ANY) ? (lab >= 0) : (lab == p.label_filter);
+      const float s = ok ? acc[reg] : -INFINITY;
+      const int row = tile * TILE_ROWS + rb + e + 8 * g + 4 * h;
+      if constexpr (COLLECT) {
+        if (s >= thr) {
+          const int pos = atomicAdd(p.cand_cnt + slot, 1);
+          if (pos < p.ccap) p.cand[(size_t)slot * p.ccap + pos] = row;
+        }
+      } else {
+        if (s > ls[KL - 1]) list_insert<KL>(ls, li, s, row);
+      }
+    }
+  };
+
+  if (my_tiles > 0) {
+    stage(0, split);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int it = 0; it < my_tiles; ++it) {
+      const int cur = it & 1;
+      const int tile = split + it * p.splits;
+      if (it + 1 < my_tiles) stage(cur ^ 1, tile + p.splits);
+      if (wave_active) {
+        f32x16 acc0 = {}, acc1 = {};
+        const char* tb = smem + cur * TILE_BYTES;
+#pragma unroll
+        for (int kk = 0; kk < KSTEPS; ++kk) {
+          const int o = offA[kk & 7] + (kk >> 3) * 256;
+          const half8 a0 = *(const half8*)(tb + o);
+          const half8 a1 = *(const half8*)(tb + o + 32 * ROW_BYTES);
+          acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, qf[kk], acc0, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, qf[kk], acc1, 0, 0, 0);
+        }
+        epilogue(acc0, cur, 0, tile);
+        epilogue(acc1, cur, 32, tile);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+  }
+
+  if constexpr (!COLLECT) {
+    // fold the partner half-wave's list (same query, other rows) into lanes 0..31
+    float ps[KL];
+    int pi[KL];
+#pragma unroll
+    for (int j = 0; j < KL; ++j) {
+      ps[j] = __shfl_xor(ls[j], 32);
+      pi[j] = __shfl_xor(li[j], 32);
+    }
+    if (h == 0 && lane_active) {
+#pragma unroll
+      for (int j = 0; j < KL; ++j)
+        if (ps[j] > ls[KL - 1]) list_insert<KL>(ls, li, ps[j], pi[j]);
+      float* os = p.part_s + ((size_t)split * p.Qp + slot) * KL;
+      int32_t* oi = p.part_i + ((size_t)split * p.Qp + slot) * KL;
+#pragma unroll
+      for (int j = 0; j < KL; ++j) {
+        os[j] = ls[j];
+        oi[j] = li[j];
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Exact rescoring helper: one wave computes q.x in f64 (fixed lane-strided order
+// + fixed butterfly => deterministic) and returns the cosine on lane 0..63.
+__device__ __forceinline__ double exact_cosine(const float* qs, double qn, const float* __restrict__ x32,
+                                               const double* __restrict__ xn, int row, int D, int DP,
+                                               int lane) {
+  const float* xr = x32 + (size_t)row * DP;
+  double acc = 0.0;
+  for (int d = lane; d < D; d += 64) acc = fma((double)qs[d], (double)xr[d], acc);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
+  const double xnr = xn[row];
+  return (qn > 0.0 && xnr > 0.0) ? acc / (qn * xnr) : 0.0;
+}
+
+struct MergeParams {
+  const float* part_s;
+  const int32_t* part_i;
+  int splits, KL, Qp, nq, k, M, R, Mp;
+  const float* q32;
+  const double* qn;
+  const float* x32;
+  const double* xn;
+  int D, DP;
+  float* out_s;
+  double* out_s64;
+  int64_t* out_r;
+  int64_t row_offset;
+  float* thresh;
+  int32_t* fail_list;
+  int32_t* fail_cnt;
+};
+
+__device__ __forceinline__ float f32_round_down(double x) {
+  float f = (float)x;
+  if ((double)f > x) f = nextafterf(f, -INFINITY);
+  return f;
+}
+
+// K8: merge split lists, rescore exactly, certify. One workgroup per query.
+__global__ __launch_bounds__(MERGE_THREADS) void knn_merge_kernel(MergeParams p) {
+  extern __shared__ __attribute__((aligned(16))) char dsm[];
+  uint64_t* keys = (uint64_t*)dsm;                                  // [R]
+  double* ex = (double*)(dsm + (size_t)p.R * 8);                    // [Mp]
+  int32_t* er = (int32_t*)(dsm + (size_t)p.R * 8 + (size_t)p.Mp * 8);  // [Mp]
+  float* qs = (float*)(dsm + (size_t)p.R * 8 + (size_t)p.Mp * 12);     // [DP]
+  float* red_f = (float*)(dsm + (size_t)p.R * 8 + (size_t)p.Mp * 12 + (size_t)p.DP * 4);  // [4]
+  int* red_i = (int*)(red_f + MERGE_THREADS / 64);                                       // [4]
+
+  const int q = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+
+  float tau = -INFINITY;
+  int valid = 0;
+  const int ntot = p.splits * p.KL;
+  for (int e = tid; e < p.R; e += MERGE_THREADS) {
+    uint64_t key = ~0ull;
+    if (e < ntot) {
+      const int sp = e / p.KL, j = e - sp * p.KL;
+      const size_t o = ((size_t)sp * p.Qp + q) * p.KL + j;
+      const int r = p.part_i[o];
+      if (r >= 0) {
+        const float s = p.part_s[o];
+        key = ((uint64_t)(~mrag_f2ord(s)) << 32) | (uint32_t)r;
+        ++valid;
+        if (j == p.KL - 1) tau = fmaxf(tau, s);
+      }
+    }
+    keys[e] = key;
+  }
+  for (int d = tid; d < p.DP; d += MERGE_THREADS) qs[d] = p.q32[(size_t)q * p.DP + d];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    tau = fmaxf(tau, __shfl_xor(tau, off));
+    valid += __shfl_xor(valid, off);
+  }
+  if (lane == 0) {
+    red_f[wave] = tau;
+    red_i[wave] = valid;
+  }
+  __syncthreads();
+  tau = red_f[0];
+  valid = red_i[0];
+  for (int i = 1; i < MERGE_THREADS / 64; ++i) {
+    tau = fmaxf(tau, red_f[i]);
+    valid += red_i[i];
+  }
+
+  // bitonic sort of keys ascending == (approx desc, row asc)
+  for (int size = 2; size <= p.R; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      __syncthreads();
+      for (int i = tid; i < (p.R >> 1); i += MERGE_THREADS) {
+        const int lo = 2 * i - (i & (stride - 1));
+        const int hi = lo + stride;
+        const bool asc = (lo & size) == 0;
+        const uint64_t a = keys[lo], b = keys[hi];
+        if ((a > b) == asc) {
+          keys[lo] = b;
+          keys[hi] = a;
+        }
+      }
+    }
+  }
+  __syncthreads();
+
+  const int M = min(p.M, valid);
+  const float a_next = (valid > M) ? mrag_ord2f(~(uint32_t)(keys[M] >> 32)) : -INFINITY;
+  const double T = (double)fmaxf(tau, a_next);
+  const double qn = p.qn[q];
+
+  for (int m = wave; m < p.Mp; m += MERGE_THREADS / 64) {
+    if (m < M) {
+      const int r = (int)(uint32_t)(keys[m] & 0xffffffffu);
+      const double s = exact_cosine(qs, qn, p.x32, p.xn, r, p.D, p.DP, lane);
+      if (lane == 0) {
+        ex[m] = s;
+        er[m] = r;
+      }
+    } else if (lane == 0) {
+      ex[m] = -INFINITY;
+      er[m] = -1;
+    }
+  }
+  // bitonic sort of (ex, er) by (score desc, row asc); empty slots last
+  for (int size = 2; size <= p.Mp; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      __syncthreads();
+      for (int i = tid; i < (p.Mp >> 1); i += MERGE_THREADS) {
+        const int lo = 2 * i - (i & (stride - 1));
+        const int hi = lo + stride;
+        const bool asc = (lo & size) == 0;
+        const double sa = ex[lo], sb = ex[hi];
+        const int ra = er[lo], rb = er[hi];
+        // "ascending" in retrieval order == a ranks before b
+        const bool b_first = mrag_before(sb, rb, sa, ra);
+        if (b_first == asc) {
+          ex[lo] = sb; er[lo] = rb;
+          ex[hi] = sa; er[hi] = ra;
+        }
+      }
+    }
+  }
+  __syncthreads();
+
+  for (int j = tid; j < p.k; j += MERGE_THREADS) {
+    const bool has = j < M;
+    const double s = has ? ex[j] : -INFINITY;
+    const size_t o = (size_t)q * p.k + j;
+    p.out_s[o] = (float)s;
+    if (p.out_s64) p.out_s64[o] = s;
+    p.out_r[o] = has ? (int64_t)er[j] + p.row_offset : -1;
+  }
+  if (tid == 0) {
+    bool cert;
+    if (tau == -INFINITY && valid <= M) {
+      cert = true;  // every matching row is in the union and was rescored
+    } else {
+      cert = (M >= p.k) && (ex[p.k - 1] > T + EPS_F16);
+    }
+    if (!cert) {
+      p.thresh[q] = (M >= p.k) ? f32_round_down(ex[p.k - 1] - EPS_F16) : -INFINITY;
+      const int s = atomicAdd(p.fail_cnt, 1);
+      p.fail_list[s] = q;
+    }
+  }
+}
+
+struct FinalParams {
+  const int32_t* fail_list;
+  const int32_t* fail_cnt;
+  const int32_t* cand_cnt;
+  const int32_t* cand;
+  int ccap;
+  double* scratch;  // [Qp][ccap]
+  const float* q32;
+  const double* qn;
+  const float* x32;
+  const double* xn;
+  int D, DP, k;
+  float* out_s;
+  double* out_s64;
+  int64_t* out_r;
+  int64_t row_offset;
+  int32_t* overflow;
+};
+
+// Block-wide "best after prev" selection step shared by K10 and K11.
+__device__ void block_select_best(double& bs, int64_t& br) {
+  __shared__ double rs[MERGE_THREADS / 64];
+  __shared__ int64_t rr[MERGE_THREADS / 64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const double os = __shfl_xor(bs, off);
+    const int64_t orr = __shfl_xor(br, off);
+    if (mrag_before(os, orr, bs, br)) {
+      bs = os;
+      br = orr;
+    }
+  }
+  __syncthreads();
+  if (lane == 0) {
+    rs[wave] = bs;
+    rr[wave] = br;
+  }
+  __syncthreads();
+  bs = rs[0];
+  br = rr[0];
+  for (int i = 1; i < MERGE_THREADS / 64; ++i)
+    if (mrag_before(rs[i], rr[i], bs, br)) {
+      bs = rs[i];
+      br = rr[i];
+    }
+}
+
+// K10: exact top-k among the rows collected for an uncertified query.
+__global__ __launch_bounds__(MERGE_THREADS) void knn_final_kernel(FinalParams p) {
+  extern __shared__ __attribute__((aligned(16))) char dsm[];
+  float* qs = (float*)dsm;
+  const int slot = blockIdx.x;
+  if (slot >= *p.fail_cnt) return;
+  const int q = p.fail_list[slot];
+  const int n = p.cand_cnt[slot];
+  if (n > p.ccap) {
+    if (threadIdx.x == 0) atomicOr(p.overflow, 1);
+    return;
+  }
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (int d = tid; d < p.DP; d += MERGE_THREADS) qs[d] = p.q32[(size_t)q * p.DP + d];
+  __syncthreads();
+  const double qn = p.qn[q];
+  double* sc = p.scratch + (size_t)slot * p.ccap;
+  const int32_t* cr = p.cand + (size_t)slot * p.ccap;
+  for (int m = wave; m < n; m += MERGE_THREADS / 64) {
+    const double s = exact_cosine(qs, qn, p.x32, p.xn, cr[m], p.D, p.DP, lane);
+    if (lane == 0) sc[m] = s;
+  }
+  __syncthreads();
+  double ps = INFINITY;
+  int64_t pr = -1;  // sentinel "before everything"
+  for (int j = 0; j < p.k; ++j) {
+    double bs = -INFINITY;
+    int64_t br = -1;
+    for (int m = tid; m < n; m += MERGE_THREADS) {
+      const double s = sc[m];
+      const int64_t r = cr[m];
+      const bool after_prev = (pr < 0) ? true : mrag_before(ps, pr, s, r);
+      if (after_prev && mrag_before(s, r, bs, br)) {
+        bs = s;
+        br = r;
+      }
+    }
+    block_select_best(bs, br);
+    if (tid == 0) {
+      const size_t o = (size_t)q * p.k + j;
+      p.out_s[o] = (float)bs;
+      if (p.out_s64) p.out_s64[o] = bs;
+      p.out_r[o] = br >= 0 ? br + p.row_offset : -1;
+    }
+    ps = bs;
+    pr = br;
+    if (br < 0) {
+      // no more rows: fill the rest
+      for (int jj = j + 1 + tid; jj < p.k; jj += MERGE_THREADS) {
+        const size_t o = (size_t)q * p.k + jj;
+        p.out_s[o] = -INFINITY;
+        if (p.out_s64) p.out_s64[o] = -INFINITY;
+        p.out_r[o] = -1;
+      }
+      break;
+    }
+  }
+}
+
+// K11: merge nlists per-shard top-k lists per query (row-sharded search).
+__global__ __launch_bounds__(MERGE_THREADS) void topk_merge_kernel(const double* __restrict__ s64,
+                                                                   const int64_t* __restrict__ rows,
+                                                                   int nlists, int64_t nq, int k,
+                                                                   float* out_s, double* out_s64,
+                                                                   int64_t* out_r) {
+  const int64_t q = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int n = nlists * k;
+  double ps = INFINITY;
+  int64_t pr = -1;
+  for (int j = 0; j < k; ++j) {
+    double bs = -INFINITY;
+    int64_t br = -1;
+    for (int m = tid; m < n; m += MERGE_THREADS) {
+      const int l = m / k, jj = m - l * k;
+      const size_t o = ((size_t)l * nq + q) * k + jj;
+      const double s = s64[o];
+      const int64_t r = rows[o];
+      if (r < 0) continue;
+      const bool after_prev = (pr < 0) ? true : mrag_before(ps, pr, s, r);
+      if (after_prev && mrag_before(s, r, bs, br)) {
+        bs = s;
+        br = r;
+      }
+    }
+    block_select_best(bs, br);
+    if (tid == 0) {
+      const size_t o = (size_t)q * k + j;
+      out_s[o] = br >= 0 ? (float)bs : -INFINITY;
+      if (out_s64) out_s64[o] = br >= 0 ? bs : -INFINITY;
+      out_r[o] = br;
+    }
+    if (br >= 0) {
+      ps = bs;
+      pr = br;
+    }
+  }
+}
+
+// Row preparation: in f32 [nin][D] -> x32 [nout][DP] (zero padded), |x| f64,
+// x16 = fp16(x/|x|). One wave per row.
+__global__ __launch_bounds__(256) void prep_rows_kernel(const float* __restrict__ in, int64_t nin,
+                                                        int D, int DP, int64_t nout,
+                                                        float* __restrict__ x32,
+                                                        double* __restrict__ xn,
+                                                        _Float16* __restrict__ x16) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= nout) return;
+  float v[8];
+  double ss = 0.0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int d = lane + 64 * j;
+    v[j] = (row < nin && d < D) ? in[row * D + d] : 0.0f;
+    ss = fma((double)v[j], (double)v[j], ss);
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) ss += __shfl_xor(ss, off);
+  const double nrm = sqrt(ss);
+  const double inv = nrm > 0.0 ? 1.0 / nrm : 0.0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int d = lane + 64 * j;
+    if (d < DP) {
+      x32[row * DP + d] = v[j];
+      x16[row * DP + d] = (_Float16)(float)((double)v[j] * inv);
+    }
+  }
+  if (lane == 0) xn[row] = nrm;
+}
+
+__global__ void fill_i32_kernel(int32_t* p, int64_t n, int32_t v) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = v;
+}
+
+__global__ void scatter_label_kernel(int32_t* labels, const int64_t* rows, int64_t n, int32_t v) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) labels[rows[i]] = v;
+}
+
+__global__ void fill_empty_kernel(float* s, double* s64, int64_t* r, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) {
+    s[i] = -INFINITY;
+    if (s64) s64[i] = -INFINITY;
+    r[i] = -1;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Host side
+// ---------------------------------------------------------------------------
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+};
+
+int ensure(DevBuf& b, size_t bytes) {
+  if (b.bytes >= bytes && b.p) return MRAG_OK;
+  if (b.p) {
+    MRAG_HIP(hipFree(b.p));
+    b.p = nullptr;
+    b.bytes = 0;
+  }
+  const size_t want = std::max<size_t>(bytes, 256);
+  MRAG_HIP(hipMalloc(&b.p, want));
+  b.bytes = want;
+  return MRAG_OK;
+}
+
+void release(DevBuf& b) {
+  if (b.p) (void)hipFree(b.p);
+  b.p = nullptr;
+  b.bytes = 0;
+}
+
+typedef void (*scan_fn)(ScanParams);
+
+template <int DP>
+scan_fn pick_scan(int KL, bool collect) {
+  if (collect) return knn_scan_kernel<DP, 8, true>;
+  // KL = 32 keeps 64 more VGPRs live; at DP >= 384 that spills, so those widths cap at 16
+  // (the certificate stays exact; only the candidate-list depth changes).
+  if (KL <= 8) return knn_scan_kernel<DP, 8, false>;
+  if (KL <= 16 || DP >= 384) return knn_scan_kernel<DP, 16, false>;
+  return knn_scan_kernel<DP, (DP >= 384 ? 16 : 32), false>;
+}
+
+scan_fn get_scan(int DP, int KL, bool collect) {
+  switch (DP) {
+    case 128: return pick_scan<128>(KL, collect);
+    case 256: return pick_scan<256>(KL, collect);
+    case 384: return pick_scan<384>(KL, collect);
+    case 512: return pick_scan<512>(KL, collect);
+    default: return nullptr;
+  }
+}
+
+int64_t next_pow2(int64_t x) {
+  int64_t p = 1;
+  while (p < x) p <<= 1;
+  return p;
+}
+
+}  // namespace
+
+struct mrag_knn_index {
+  std::mutex mu;
+  int device = 0;
+  int D = 0, DP = 0;
+  int64_t n = 0, cap = 0;
+  DevBuf x16, x32, xn, labels;
+  hipStream_t stream = nullptr;
+  // search workspace
+  DevBuf qin, q32, qn, q16, part_s, part_i, thresh, fail_list, counters, cand_cnt, cand, scratch;
+  DevBuf out_s, out_s64, out_r, stage_rows, stage_labels, rowlist;
+  int32_t* host_counters = nullptr;  // pinned [2]: fail_cnt, overflow
+  int ccap = 4096;
+  int64_t last_uncertified = 0, last_retries = 0;
+  // optional scan timing (mrag_knn_profile)
+  bool profile = false;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  double scan_ms = 0.0;
+  int64_t scan_launches = 0;
+};
+
+namespace {
+
+int grow(mrag_knn_index* ix, int64_t need) {
+  if (need <= ix->cap) return MRAG_OK;
+  int64_t ncap = std::max<int64_t>({(int64_t)TILE_ROWS, ix->cap * 2, need});
+  ncap = (ncap + TILE_ROWS - 1) / TILE_ROWS * TILE_ROWS;
+  DevBuf nx16, nx32, nxn, nlab;
+  if (int rc = ensure(nx16, (size_t)ncap * ix->DP * 2)) return rc;
+  if (int rc = ensure(nx32, (size_t)ncap * ix->DP * 4)) return rc;
+  if (int rc = ensure(nxn, (size_t)ncap * 8)) return rc;
+  if (int rc = ensure(nlab, (size_t)ncap * 4)) return rc;
+  hipStream_t s = ix->stream;
+  MRAG_HIP(hipMemsetAsync(nx16.p, 0, (size_t)ncap * ix->DP * 2, s));
+  MRAG_HIP(hipMemsetAsync(nx32.p, 0, (size_t)ncap * ix->DP * 4, s));
+  MRAG_HIP(hipMemsetAsync(nxn.p, 0, (size_t)ncap * 8, s));
+  hipLaunchKernelGGL(fill_i32_kernel, dim3((unsigned)((ncap + 255) / 256)), dim3(256), 0, s,
+                     (int32_t*)nlab.p, ncap, (int32_t)MRAG_LABEL_DELETED);
+  MRAG_CHECK_LAUNCH();
+  if (ix->n > 0) {
+    MRAG_HIP(hipMemcpyAsync(nx16.p, ix->x16.p, (size_t)ix->n * ix->DP * 2, hipMemcpyDeviceToDevice, s));
+    MRAG_HIP(hipMemcpyAsync(nx32.p, ix->x32.p, (size_t)ix->n * ix->DP * 4, hipMemcpyDeviceToDevice, s));
+    MRAG_HIP(hipMemcpyAsync(nxn.p, ix->xn.p, (size_t)ix->n * 8, hipMemcpyDeviceToDevice, s));
+    MRAG_HIP(hipMemcpyAsync(nlab.p, ix->labels.p, (size_t)ix->n * 4, hipMemcpyDeviceToDevice, s));
+  }
+  MRAG_HIP(hipStreamSynchronize(s));
+  release(ix->x16);
+  release(ix->x32);
+  release(ix->xn);
+  release(ix->labels);
+  ix->x16 = nx16;
+  ix->x32 = nx32;
+  ix->xn = nxn;
+  ix->labels = nlab;
+  ix->cap = ncap;
+  return MRAG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mrag_knn_create(int32_t dim, int32_t device, mrag_knn_index** out) {
+  MRAG_REQUIRE(out != nullptr, "out is NULL");
+  *out = nullptr;
+  MRAG_REQUIRE(dim >= 1 && dim <= 512, "dim %d unsupported (1..512)", dim);
+  int ndev = 0;
+  MRAG_HIP(hipGetDeviceCount(&ndev));
+  MRAG_REQUIRE(device >= 0 && device < ndev, "device %d out of range (%d devices)", device, ndev);
+  mrag::DeviceGuard g(device);
+  auto* ix = new mrag_knn_index();
+  ix->device = device;
+  ix->D = dim;
+  ix->DP = (dim + 127) / 128 * 128;
+  hipError_t e = hipStreamCreateWithFlags(&ix->stream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipHostMalloc((void**)&ix->host_counters, 16, hipHostMallocDefault);
+  if (e != hipSuccess) {
+    delete ix;
+    return mrag::fail(MRAG_ERR_HIP, "stream/pinned alloc: %s", hipGetErrorString(e));
+  }
+  *out = ix;
+  return MRAG_OK;
+}
+
+int mrag_knn_destroy(mrag_knn_index* ix) {
+  if (!ix) return MRAG_OK;
+  {
+    mrag::DeviceGuard g(ix->device);
+    (void)hipStreamSynchronize(ix->stream);
+    for (DevBuf* b : {&ix->x16, &ix->x32, &ix->xn, &ix->labels, &ix->qin, &ix->q32, &ix->qn, &ix->q16,
+                      &ix->part_s, &ix->part_i, &ix->thresh, &ix->fail_list, &ix->counters,
+                      &ix->cand_cnt, &ix->cand, &ix->scratch, &ix->out_s, &ix->out_s64, &ix->out_r,
+                      &ix->stage_rows, &ix->stage_labels, &ix->rowlist})
+      release(*b);
+    if (ix->host_counters) (void)hipHostFree(ix->host_counters);
+    if (ix->ev0) (void)hipEventDestroy(ix->ev0);
+    if (ix->ev1) (void)hipEventDestroy(ix->ev1);
+    if (ix->stream) (void)hipStreamDestroy(ix->stream);
+  }
+  delete ix;
+  return MRAG_OK;
+}
+
+int mrag_knn_size(const mrag_knn_index* ix, int64_t* n) {
+  MRAG_REQUIRE(ix != nullptr && n != nullptr, "NULL argument");
+  *n = ix->n;
+  return MRAG_OK;
+}
+
+int mrag_knn_last_stats(const mrag_knn_index* ix, int64_t* uncertified, int64_t* retries) {
+  MRAG_REQUIRE(ix != nullptr, "NULL index");
+  if (uncertified) *uncertified = ix->last_uncertified;
+  if (retries) *retries = ix->last_retries;
+  return MRAG_OK;
+}
+
+int mrag_knn_profile(mrag_knn_index* ix, int32_t enable, double* scan_ms_total, int64_t* scan_launches) {
+  MRAG_REQUIRE(ix != nullptr, "NULL index");
+  std::lock_guard<std::mutex> lk(ix->mu);
+  mrag::DeviceGuard g(ix->device);
+  if (enable == 1) {
+    if (!ix->ev0) MRAG_HIP(hipEventCreate(&ix->ev0));
+    if (!ix->ev1) MRAG_HIP(hipEventCreate(&ix->ev1));
+    ix->profile = true;
+    ix->scan_ms = 0.0;
+    ix->scan_launches = 0;
+  } else if (enable == 0) {
+    ix->profile = false;
+  }
+  if (scan_ms_total) *scan_ms_total = ix->scan_ms;
+  if (scan_launches) *scan_launches = ix->scan_launches;
+  return MRAG_OK;
+}
+
+int mrag_knn_add(mrag_knn_index* ix, const float* rows, const int32_t* labels, int64_t nrows,
+                 int32_t ptr_kind, int64_t* first_row) {
+  MRAG_REQUIRE(ix != nullptr, "NULL index");
+  MRAG_REQUIRE(nrows >= 0, "negative row count");
+  MRAG_REQUIRE(ptr_kind == MRAG_PTR_HOST || ptr_kind == MRAG_PTR_DEVICE, "bad ptr_kind %d", ptr_kind);
+  std::lock_guard<std::mutex> lk(ix->mu);
+  mrag::DeviceGuard g(ix->device);
+  if (first_row) *first_row = ix->n;
+  if (nrows == 0) return MRAG_OK;
+  MRAG_REQUIRE(rows != nullptr && labels != nullptr, "NULL rows/labels");
+  MRAG_REQUIRE(ix->n + nrows < (int64_t)1 << 31, "index would exceed 2^31 rows per shard");
+  if (int rc = grow(ix, ix->n + nrows)) return rc;
+  hipStream_t s = ix->stream;
+  const float* src = rows;
+  const int32_t* lsrc = labels;
+  if (ptr_kind == MRAG_PTR_HOST) {
+    if (int rc = ensure(ix->stage_rows, (size_t)nrows * ix->D * 4)) return rc;
+    if (int rc = ensure(ix->stage_labels, (size_t)nrows * 4)) return rc;
+    MRAG_HIP(hipMemcpyAsync(ix->stage_rows.p, rows, (size_t)nrows * ix->D * 4, hipMemcpyHostToDevice, s));
+    MRAG_HIP(hipMemcpyAsync(ix->stage_labels.p, labels, (size_t)nrows * 4, hipMemcpyHostToDevice, s));
+    src = (const float*)ix->stage_rows.p;
+    lsrc = (const int32_t*)ix->stage_labels.p;
+  }
+  const int64_t n0 = ix->n;
+  hipLaunchKernelGGL(prep_rows_kernel, dim3((unsigned)((nrows + 3) / 4)), dim3(256), 0, s, src, nrows,
+                     ix->D, ix->DP, nrows, (float*)ix->x32.p + n0 * ix->DP, (double*)ix->xn.p + n0,
+                     (_Float16*)ix->x16.p + n0 * ix->DP);
+  MRAG_CHECK_LAUNCH();
+  MRAG_HIP(hipMemcpyAsync((int32_t*)ix->labels.p + n0, lsrc, (size_t)nrows * 4, hipMemcpyDeviceToDevice, s));
+  MRAG_HIP(hipStreamSynchronize(s));
+  ix->n += nrows;
+  return MRAG_OK;
+}
+
+int mrag_knn_set_labels(mrag_knn_index* ix, const int64_t* rows, int64_t n, int32_t label) {
+  MRAG_REQUIRE(ix != nullptr, "NULL index");
+  MRAG_REQUIRE(n >= 0, "negative count");
+  MRAG_REQUIRE(label >= 0 || label == MRAG_LABEL_DELETED, "label %d invalid", label);
+  std::lock_guard<std::mutex> lk(ix->mu);
+  mrag::DeviceGuard g(ix->device);
+  if (n == 0) return MRAG_OK;
+  MRAG_REQUIRE(rows != nullptr, "NULL rows");
+  for (int64_t i = 0; i < n; ++i)
+    MRAG_REQUIRE(rows[i] >= 0 && rows[i] < ix->n, "row %lld out of range [0,%lld)", (long long)rows[i],
+                 (long long)ix->n);
+  if (int rc = ensure(ix->rowlist, (size_t)n * 8)) return rc;
+  MRAG_HIP(hipMemcpyAsync(ix->rowlist.p, rows, (size_t)n * 8, hipMemcpyHostToDevice, ix->stream));
+  hipLaunchKernelGGL(scatter_label_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ix->stream,
+                     (int32_t*)ix->labels.p, (const int64_t*)ix->rowlist.p, n, label);
+  MRAG_CHECK_LAUNCH();
+  MRAG_HIP(hipStreamSynchronize(ix->stream));
+  return MRAG_OK;
+}
+
+int mrag_knn_search(mrag_knn_index* ix, const float* queries, int64_t nq, int32_t k,
+                    int32_t label_filter, int64_t row_offset, float* out_scores, double* out_scores64,
+                    int64_t* out_rows, int32_t ptr_kind, void* stream_arg) {
+  MRAG_REQUIRE(ix != nullptr, "NULL index");
+  MRAG_REQUIRE(nq >= 0, "negative query count");
+  MRAG_REQUIRE(k >= 1 && k <= MAX_K, "k=%d unsupported (1..%d)", k, MAX_K);
+  MRAG_REQUIRE(label_filter >= MRAG_LABEL_ANY, "label filter %d invalid", label_filter);
+  MRAG_REQUIRE(ptr_kind == MRAG_PTR_HOST || ptr_kind == MRAG_PTR_DEVICE, "bad ptr_kind %d", ptr_kind);
+  MRAG_REQUIRE(nq < (1 << 24), "too many queries in one call");
+  std::lock_guard<std::mutex> lk(ix->mu);
+  mrag::DeviceGuard g(ix->device);
+  if (nq == 0) return MRAG_OK;
+  MRAG_REQUIRE(queries && out_scores && out_rows, "NULL query/output pointer");
+  hipStream_t s = stream_arg ? (hipStream_t)stream_arg : ix->stream;
+  const bool host = ptr_kind == MRAG_PTR_HOST;
+  const int D = ix->D, DP = ix->DP;
+  const int64_t nout = nq * k;
+
+  // output destinations (device)
+  float* os = out_scores;
+  double* os64 = out_scores64;
+  int64_t* orr = out_rows;
+  if (host) {
+    if (int rc = ensure(ix->out_s, nout * 4)) return rc;
+    if (int rc = ensure(ix->out_r, nout * 8)) return rc;
+    os = (float*)ix->out_s.p;
+    orr = (int64_t*)ix->out_r.p;
+    if (out_scores64) {
+      if (int rc = ensure(ix->out_s64, nout * 8)) return rc;
+      os64 = (double*)ix->out_s64.p;
+    }
+  }
+  ix->last_uncertified = 0;
+  ix->last_retries = 0;
+
+  if (ix->n == 0) {
+    hipLaunchKernelGGL(fill_empty_kernel, dim3((unsigned)((nout + 255) / 256)), dim3(256), 0, s, os, os64,
+                       orr, nout);
+    MRAG_CHECK_LAUNCH();
+  } else {
+    const int64_t Qp = (nq + QPW - 1) / QPW * QPW;
+    const int qgroups = (int)((Qp + QPG - 1) / QPG);
+    const int ntiles = (int)((ix->n + TILE_ROWS - 1) / TILE_ROWS);
+    const int KL = k <= 8 ? 8 : ((k <= 16 || DP >= 384) ? 16 : 32);
+    int S = std::max(1, 256 / qgroups);
+    S = std::min(S, ntiles);
+    S = std::min(S, MAX_MERGE_ENTRIES / KL);
+    if (S >= 8) S &= ~7;
+    const int M = std::min<int>(k + 32, S * KL);
+    const int R = (int)next_pow2((int64_t)S * KL);
+    const int Mp = (int)next_pow2(std::max(M, 2));
+
+    const float* qsrc = queries;
+    if (host) {
+      if (int rc = ensure(ix->qin, (size_t)nq * D * 4)) return rc;
+      MRAG_HIP(hipMemcpyAsync(ix->qin.p, queries, (size_t)nq * D * 4, hipMemcpyHostToDevice, s));
+      qsrc = (const float*)ix->qin.p;
+    }
+    if (int rc = ensure(ix->q32, (size_t)Qp * DP * 4)) return rc;
+    if (int rc = ensure(ix->qn, (size_t)Qp * 8)) return rc;
+    if (int rc = ensure(ix->q16, (size_t)Qp * DP * 2)) return rc;
+    if (int rc = ensure(ix->part_s, (size_t)S * Qp * KL * 4)) return rc;
+    if (int rc = ensure(ix->part_i, (size_t)S * Qp * KL * 4)) return rc;
+    if (int rc = ensure(ix->thresh, (size_t)Qp * 4)) return rc;
+    if (int rc = ensure(ix->fail_list, (size_t)Qp * 4)) return rc;
+    if (int rc = ensure(ix->counters, 16)) return rc;
+    if (int rc = ensure(ix->cand_cnt, (size_t)Qp * 4)) return rc;
+
+    hipLaunchKernelGGL(prep_rows_kernel, dim3((unsigned)((Qp + 3) / 4)), dim3(256), 0, s, qsrc, nq, D, DP,
+                       Qp, (float*)ix->q32.p, (double*)ix->qn.p, (_Float16*)ix->q16.p);
+    MRAG_CHECK_LAUNCH();
+    MRAG_HIP(hipMemsetAsync(ix->counters.p, 0, 16, s));
+    MRAG_HIP(hipMemsetAsync(ix->cand_cnt.p, 0, (size_t)Qp * 4, s));
+
+    ScanParams sp{};
+    sp.x16 = (const _Float16*)ix->x16.p;
+    sp.labels = (const int32_t*)ix->labels.p;
+    sp.q16 = (const _Float16*)ix->q16.p;
+    sp.ntiles = ntiles;
+    sp.qgroups = qgroups;
+    sp.splits = S;
+    sp.Qp = (int)Qp;
+    sp.label_filter = label_filter;
+    sp.part_s = (float*)ix->part_s.p;
+    sp.part_i = (int32_t*)ix->part_i.p;
+    sp.fail_list = (const int32_t*)ix->fail_list.p;
+    sp.fail_cnt = (const int32_t*)ix->counters.p;
+    sp.thresh = (const float*)ix->thresh.p;
+    sp.cand_cnt = (int32_t*)ix->cand_cnt.p;
+
+    scan_fn scan = get_scan(DP, KL, false);
+    scan_fn collect = get_scan(DP, 8, true);
+    if (!scan || !collect) return mrag::fail(MRAG_ERR_UNSUPPORTED, "no scan kernel for DP=%d", DP);
+    const dim3 sgrid((unsigned)(qgroups * S));
+    if (ix->profile) MRAG_HIP(hipEventRecord(ix->ev0, s));
+    hipLaunchKernelGGL(scan, sgrid, dim3(SCAN_THREADS), 0, s, sp);
+    MRAG_CHECK_LAUNCH();
+    if (ix->profile) MRAG_HIP(hipEventRecord(ix->ev1, s));
+
+    MergeParams mp{};
+    mp.part_s = sp.part_s;
+    mp.part_i = sp.part_i;
+    mp.splits = S;
+    mp.KL = KL;
+    mp.Qp = (int)Qp;
+    mp.nq = (int)nq;
+    mp.k = k;
+    mp.M = M;
+    mp.R = R;
+    mp.Mp = Mp;
+    mp.q32 = (const float*)ix->q32.p;
+    mp.qn = (const double*)ix->qn.p;
+    mp.x32 = (const float*)ix->x32.p;
+    mp.xn = (const double*)ix->xn.p;
+    mp.D = D;
+    mp.DP = DP;
+    mp.out_s = os;
+    mp.out_s64 = os64;
+    mp.out_r = orr;
+    mp.row_offset = row_offset;
+    mp.thresh = (float*)ix->thresh.p;
+    mp.fail_list = (int32_t*)ix->fail_list.p;
+    mp.fail_cnt = (int32_t*)ix->counters.p;
+    const size_t msh = (size_t)R * 8 + (size_t)Mp * 12 + (size_t)DP * 4 + 64;
+    hipLaunchKernelGGL(knn_merge_kernel, dim3((unsigned)nq), dim3(MERGE_THREADS), msh, s, mp);
+    MRAG_CHECK_LAUNCH();
+
+    for (int attempt = 0;; ++attempt) {
+      if (int rc = ensure(ix->cand, (size_t)Qp * ix->ccap * 4)) return rc;
+      if (int rc = ensure(ix->scratch, (size_t)Qp * ix->ccap * 8)) return rc;
+      sp.cand = (int32_t*)ix->cand.p;
+      sp.ccap = ix->ccap;
+      hipLaunchKernelGGL(collect, sgrid, dim3(SCAN_THREADS), 0, s, sp);
+      MRAG_CHECK_LAUNCH();
+      FinalParams fp{};
+      fp.fail_list = sp.fail_list;
+      fp.fail_cnt = sp.fail_cnt;
+      fp.cand_cnt = sp.cand_cnt;
+      fp.cand = sp.cand;
+      fp.ccap = ix->ccap;
+      fp.scratch = (double*)ix->scratch.p;
+      fp.q32 = mp.q32;
+      fp.qn = mp.qn;
+      fp.x32 = mp.x32;
+      fp.xn = mp.xn;
+      fp.D = D;
+      fp.DP = DP;
+      fp.k = k;
+      fp.out_s = os;
+      fp.out_s64 = os64;
+      fp.out_r = orr;
+      fp.row_offset = row_offset;
+      fp.overflow = (int32_t*)ix->counters.p + 1;
+      hipLaunchKernelGGL(knn_final_kernel, dim3((unsigned)nq), dim3(MERGE_THREADS), (size_t)DP * 4, s, fp);
+      MRAG_CHECK_LAUNCH();
+      MRAG_HIP(hipMemcpyAsync(ix->host_counters, ix->counters.p, 8, hipMemcpyDeviceToHost, s));
+      MRAG_HIP(hipStreamSynchronize(s));
+      ix->last_uncertified = ix->host_counters[0];
+      if (ix->profile && attempt == 0) {
+        float ms = 0.f;
+        MRAG_HIP(hipEventElapsedTime(&ms, ix->ev0, ix->ev1));
+        ix->scan_ms += ms;
+        ix->scan_launches++;
+      }
+      if (ix->host_counters[1] == 0) break;
+      // some uncertified query collected more rows than ccap: size for the worst one and rerun
+      std::vector<int32_t> cnt((size_t)ix->host_counters[0]);
+      MRAG_HIP(hipMemcpy(cnt.data(), ix->cand_cnt.p, cnt.size() * 4, hipMemcpyDeviceToHost));
+      int mx = 0;
+      for (int32_t c : cnt) mx = std::max(mx, c);
+      MRAG_REQUIRE(attempt < 3, "collect pass did not converge");
+      ix->ccap = (mx + 1023) / 1024 * 1024;
+      ix->last_retries++;
+      MRAG_HIP(hipMemsetAsync(ix->cand_cnt.p, 0, (size_t)Qp * 4, s));
+      MRAG_HIP(hipMemsetAsync((int32_t*)ix->counters.p + 1, 0, 4, s));
+    }
+  }
+
+  if (host) {
+    MRAG_HIP(hipMemcpyAsync(out_scores, os, nout * 4, hipMemcpyDeviceToHost, s));
+    MRAG_HIP(hipMemcpyAsync(out_rows, orr, nout * 8, hipMemcpyDeviceToHost, s));
+    if (out_scores64) MRAG_HIP(hipMemcpyAsync(out_scores64, os64, nout * 8, hipMemcpyDeviceToHost, s));
+  }
+  MRAG_HIP(hipStreamSynchronize(s));
+  return MRAG_OK;
+}
+
+int mrag_topk_merge(const double* scores64, const int64_t* rows, int32_t nlists, int64_t nq, int32_t k,
+                    float* out_scores, double* out_scores64, int64_t* out_rows, void* stream) {
+  MRAG_REQUIRE(nlists >= 1 && nq >= 0 && k >= 1 && k <= MAX_K, "bad shape nlists=%d nq=%lld k=%d", nlists,
+               (long long)nq, k);
+  if (nq == 0) return MRAG_OK;
+  MRAG_REQUIRE(scores64 && rows && out_scores && out_rows, "NULL pointer");
+  MRAG_REQUIRE(nq < (1ll << 31), "too many queries");
+  hipLaunchKernelGGL(topk_merge_kernel, dim3((unsigned)nq), dim3(MERGE_THREADS), 0, (hipStream_t)stream,
+                     scores64, rows, nlists, nq, k, out_scores, out_scores64, out_rows);
+  MRAG_CHECK_LAUNCH();
+  return MRAG_OK;
+}
+
+}  // extern "C"

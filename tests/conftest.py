@@ -1,0 +1,36 @@
+"""Test configuration: markers, import paths, shared fixtures.
+
+``-m "not gpu"`` (CPU, here): oracle vs golden vectors, host logic, C-ABI exports.
+``-m gpu`` (MI355X box): parity of the HIP path (through the C ABI) against the oracle.
+GPU tests never skip on a missing GPU — they fail, so a broken box cannot pass.
+"""
+from __future__ import annotations
+
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "multimodal-rag-for-image-text-search_amd")
+for p in (PKG, ROOT):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP path through libmrag.so)")
+    config.addinivalue_line("markers", "slow: long-running CPU test")
+
+
+@pytest.fixture(scope="session")
+def cuda():
+    import torch
+
+    assert torch.cuda.is_available(), "GPU test on a machine without a visible GPU"
+    from app import _native
+
+    _native.load()
+    return torch.device("cuda:0")

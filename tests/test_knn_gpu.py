@@ -1,0 +1,189 @@
+"""Parity of the HIP kNN path (libmrag.so via the C ABI) with the oracle.
+
+Bar (BASELINE.json north_star): bit-exact top-k rows on identical f32 embeddings,
+cosine scores within 1e-4 — here scores are checked to 1e-6 (f32 rounding of the
+same f64 value). Covers the edge cases the domain has: label prefilter, deleted
+rows, exact duplicates (ties -> row asc), near-duplicate clusters (certificate
+fails -> threshold-collect pass), zero vectors, k > matches, empty index, odd dims,
+host and device pointers, sharded merge, and the full 1M x 512 configuration.
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from _data import clustered_corpus, labels_for, unit_rows
+from oracle.knn import flat_cosine_topk
+
+pytestmark = pytest.mark.gpu
+
+SCORE_TOL = 1e-6
+
+
+def _check(gs, gr, os_, or_):
+    gs = np.asarray(gs)
+    gr = np.asarray(gr)
+    assert gr.shape == or_.shape
+    np.testing.assert_array_equal(gr, or_)
+    valid = or_ >= 0
+    assert np.all(np.isneginf(gs[~valid]))
+    np.testing.assert_allclose(gs[valid], os_[valid].astype(np.float32), rtol=0, atol=SCORE_TOL)
+
+
+def test_random_512_k10(cuda):
+    from app.vector_store import FlatIndex
+
+    x = unit_rows(20000, 512, 1)
+    q = unit_rows(100, 512, 2)
+    ix = FlatIndex(512)
+    assert ix.add(x) == 0
+    s, r = ix.search(q, 10)
+    os_, or_ = flat_cosine_topk(x, np.zeros(len(x)), q, 10)
+    _check(s, r, os_, or_)
+    unc, _ = ix.last_stats()
+    assert unc == 0  # random data: the fp16 certificate always holds
+
+
+@pytest.mark.parametrize("dim,k,nq", [(384, 50, 33), (384, 12, 1), (100, 1, 1), (256, 20, 70), (512, 16, 257)])
+def test_dims_k_filter(cuda, dim, k, nq):
+    from app.vector_store import FlatIndex
+
+    n = 9000
+    x = unit_rows(n, dim, 10 + dim) * np.float32(3.0)  # un-normalised rows are fine
+    lab = labels_for(n, 7, 5)
+    q = unit_rows(nq, dim, 11 + dim)
+    ix = FlatIndex(dim)
+    ix.add(x, lab)
+    for f in (-1, 0, 3):
+        s, r = ix.search(q, k, label=f)
+        os_, or_ = flat_cosine_topk(x, lab, q, k, label_filter=f)
+        _check(s, r, os_, or_)
+
+
+def test_clusters_duplicates_ties(cuda):
+    """Near-duplicate clusters + exact duplicate rows: exercises ties and the
+    uncertified -> threshold-collect path."""
+    from app.vector_store import FlatIndex
+
+    x = clustered_corpus(30000, 512, 7, n_clusters=8, spread=0.01, dup_frac=0.2)
+    q = x[np.random.default_rng(3).integers(0, len(x), 48)] + 0.001
+    ix = FlatIndex(512)
+    ix.add(x)
+    for k in (10, 50):
+        s, r = ix.search(q, k)
+        os_, or_ = flat_cosine_topk(x, np.zeros(len(x)), q, k)
+        _check(s, r, os_, or_)
+    unc, _ = ix.last_stats()
+    assert unc > 0, "expected the dense clusters to defeat the fp16 certificate"
+
+
+def test_many_exact_ties_overflow_retry(cuda):
+    """5000 identical rows: the collect pass must grow past its default capacity."""
+    from app.vector_store import FlatIndex
+
+    base = unit_rows(1, 128, 9)
+    x = np.concatenate([np.repeat(base, 5000, 0), unit_rows(3000, 128, 8)])
+    ix = FlatIndex(128)
+    ix.add(x)
+    s, r = ix.search(base, 10)
+    np.testing.assert_array_equal(r[0], np.arange(10))
+    assert np.allclose(s[0], 1.0, atol=1e-6)
+
+
+def test_edges_empty_deleted_zero(cuda):
+    from app.vector_store import FlatIndex
+
+    ix = FlatIndex(64)
+    s, r = ix.search(unit_rows(3, 64, 1), 5)  # empty index
+    assert np.all(r == -1) and np.all(np.isneginf(s))
+    x = unit_rows(5, 64, 2)
+    x[2] = 0.0  # zero row scores 0
+    ix.add(x, np.array([0, 0, 0, 1, 1]))
+    q = unit_rows(2, 64, 3)
+    s, r = ix.search(q, 10)  # k > rows
+    os_, or_ = flat_cosine_topk(x, np.array([0, 0, 0, 1, 1]), q, 10)
+    _check(s, r, os_, or_)
+    ix.delete([0, 3])
+    lab = np.array([-2, 0, 0, -2, 1])
+    for f in (-1, 0, 1, 5):
+        s, r = ix.search(q, 3, label=f)
+        os_, or_ = flat_cosine_topk(x, lab, q, 3, label_filter=f)
+        _check(s, r, os_, or_)
+    s, r = ix.search(np.zeros((1, 64), np.float32), 3)  # zero query: every score 0, row order
+    np.testing.assert_array_equal(r[0], [1, 2, 4])
+    assert np.all(s[0] == 0.0)
+
+
+def test_device_pointers_and_offset(cuda):
+    import torch
+    from app.vector_store import FlatIndex
+
+    x = unit_rows(5000, 512, 21)
+    q = unit_rows(40, 512, 22)
+    ix = FlatIndex(512)
+    ix.add(torch.from_numpy(x).to(cuda))
+    s, r, s64 = ix.search(torch.from_numpy(q).to(cuda), 10, row_offset=1000, with_f64=True)
+    os_, or_ = flat_cosine_topk(x, np.zeros(len(x)), q, 10, row_offset=1000)
+    _check(s.cpu().numpy(), r.cpu().numpy(), os_, or_)
+    np.testing.assert_allclose(s64.cpu().numpy(), os_, rtol=0, atol=1e-12)
+
+
+def test_sharded_merge_equals_single(cuda):
+    import torch
+    from app.vector_store import FlatIndex, topk_merge
+
+    x = clustered_corpus(12000, 384, 31, dup_frac=0.1)
+    q = unit_rows(64, 384, 32)
+    k = 10
+    shards = np.array_split(np.arange(len(x)), 4)
+    lists_s, lists_r = [], []
+    for sh in shards:
+        ix = FlatIndex(384)
+        ix.add(x[sh])
+        s, r, s64 = ix.search(torch.from_numpy(q).to(cuda), k, row_offset=int(sh[0]), with_f64=True)
+        lists_s.append(s64)
+        lists_r.append(r)
+    ms, mr, _ = topk_merge(torch.stack(lists_s), torch.stack(lists_r), k)
+    os_, or_ = flat_cosine_topk(x, np.zeros(len(x)), q, k)
+    _check(ms.cpu().numpy(), mr.cpu().numpy(), os_, or_)
+
+
+def test_l2norm_bit_exact(cuda):
+    import torch
+    from app.vector_store import l2norm_rows
+
+    rng = np.random.default_rng(0)
+    for d in (384, 512, 7, 300):
+        x = (rng.standard_normal((257, d)) * rng.uniform(0.01, 50, (257, 1))).astype(np.float32)
+        x[3] = 0.0
+        ref = x / np.where(np.linalg.norm(x, axis=1, keepdims=True) == 0, 1.0,
+                           np.linalg.norm(x, axis=1, keepdims=True))
+        got = l2norm_rows(torch.from_numpy(x).to(cuda)).cpu().numpy()
+        np.testing.assert_array_equal(got, ref.astype(np.float32))
+
+
+def test_full_size_1m_x_512(cuda):
+    """BASELINE config 3 shape: 1M x 512 corpus, 1000 queries, k=10. Every query is
+    checked for sortedness and self-consistency; 32 sampled queries against the
+    exact oracle."""
+    import torch
+    from app.vector_store import FlatIndex
+
+    g = torch.Generator(device=cuda).manual_seed(0)
+    x = torch.randn((1 << 20, 512), generator=g, device=cuda)
+    x = x / x.norm(dim=1, keepdim=True)
+    q = torch.randn((1000, 512), generator=g, device=cuda)
+    ix = FlatIndex(512)
+    ix.add(x)
+    s, r, s64 = ix.search(q, 10, with_f64=True)
+    s64 = s64.cpu().numpy()
+    r = r.cpu().numpy()
+    assert np.all(r >= 0)
+    assert np.all(np.diff(s64, axis=1) <= 0)
+    xh = x.cpu().numpy()
+    qh = q.cpu().numpy()
+    sel = np.arange(0, 1000, 1000 // 32)[:32]
+    os_, or_ = flat_cosine_topk(xh, np.zeros(len(xh)), qh[sel], 10)
+    _check(s.cpu().numpy()[sel], r[sel], os_, or_)
+    unc, _ = ix.last_stats()
+    assert unc == 0
