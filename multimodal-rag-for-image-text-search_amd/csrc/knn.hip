@@ -26,6 +26,7 @@
 //   xn     [cap]     f64    |x|
 //   labels [cap]     int32  user label, MRAG_LABEL_DELETED for tombstones / padding
 #include <algorithm>
+#include <cstdlib>
 #include <mutex>
 #include <vector>
 
@@ -66,6 +67,8 @@ struct ScanParams {
   int32_t* cand_cnt;
   int32_t* cand;
   int ccap;
+  // shared per-query rejection threshold (ordered-uint f32, 0 == none), top-k mode
+  uint32_t* theta;
 };
 
 template <int KL>
@@ -84,12 +87,62 @@ __device__ __forceinline__ void list_insert(float (&ls)[KL], int (&li)[KL], floa
   }
 }
 
+// LDS-DMA through inline asm: hipcc cannot prove that ds_reads of the current tile
+// do not alias the in-flight DMA into the other buffer and would otherwise put an
+// `s_waitcnt vmcnt(0)` right behind every builtin global_load_lds (serialising load
+// and compute). Completion is enforced by hand: `s_waitcnt vmcnt(0)` + barrier at
+// the end of every tile, before the buffer is read.
+__device__ __forceinline__ void glds_x4(const void* gsrc, uint32_t lds_addr) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(lds_addr)
+      : "memory");
+}
+__device__ __forceinline__ void glds_x1(const void* gsrc, uint32_t lds_addr) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(lds_addr)
+      : "memory");
+}
+
+__device__ __forceinline__ float max16(const f32x16& a) {
+  float m0 = fmaxf(fmaxf(a[0], a[1]), fmaxf(a[2], a[3]));
+  float m1 = fmaxf(fmaxf(a[4], a[5]), fmaxf(a[6], a[7]));
+  float m2 = fmaxf(fmaxf(a[8], a[9]), fmaxf(a[10], a[11]));
+  float m3 = fmaxf(fmaxf(a[12], a[13]), fmaxf(a[14], a[15]));
+  return fmaxf(fmaxf(m0, m1), fmaxf(m2, m3));
+}
+
+// Row validity of accumulator register `reg` of block `blk` for this lane: bit
+// (blk*32 + 8*(reg>>2) + (reg&3)) of the lane-shifted tile mask.
+__device__ __forceinline__ bool row_ok(uint64_t lane_mask, int blk, int reg) {
+  return (lane_mask >> (blk * 32 + 8 * (reg >> 2) + (reg & 3))) & 1ull;
+}
+
+__device__ __forceinline__ float masked_max16(const f32x16& a, uint64_t lane_mask, int blk) {
+  float m = -INFINITY;
+#pragma unroll
+  for (int reg = 0; reg < 16; ++reg) m = fmaxf(m, row_ok(lane_mask, blk, reg) ? a[reg] : -INFINITY);
+  return m;
+}
+
 // K7 / K7c. One workgroup = 8 waves = 256 queries x one split of the corpus tiles
 // (tiles split, split+S, split+2S, ...). Corpus tiles (64 rows) are double-buffered in
-// LDS by global_load_lds (16 B/lane, rows XOR-swizzled on the source address so the
+// LDS by LDS-DMA (16 B/lane, rows XOR-swizzled on the source address so the
 // A-fragment ds_read_b128 is conflict-free); each wave keeps its 32 queries' B
-// fragments (all of DP) in VGPRs for the whole launch.
-template <int DP, int KL, bool COLLECT>
+// fragments (all of DP) in VGPRs for the whole launch. MFMA 32x32x16 f16 with the
+// corpus rows as A (M) and the queries as B (N): lane l owns query l&31 and rows
+// (r&3) + 8(r>>2) + 4(l>>5) of each 32-row block.
+//
+// Epilogue (top-k mode): the common case is branch-free — a per-tile row-validity
+// mask from one ballot over the tile's labels, the max of each lane's 32 scores,
+// and ONE wave-level test against the lane's rejection threshold; the per-row list
+// insertion runs only when some lane of the wave has a score above its threshold.
+template <int DP, int KL, bool COLLECT, bool ABLATE = false>
 __global__ __launch_bounds__(SCAN_THREADS) void knn_scan_kernel(ScanParams p) {
   constexpr int KSTEPS = DP / 16;
   constexpr int ROW_BYTES = DP * 2;
@@ -105,6 +158,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void knn_scan_kernel(ScanParams p) {
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int h = lane >> 5;
   const int r32 = lane & 31;
+  const uint32_t lds_base = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)((AS3 char*)smem));
 
   // block -> (query group, split). Blocks b, b+8, b+16, ... share an XCD (observed
   // round-robin dispatch; speed only): the query groups of one split are placed in
@@ -138,10 +192,15 @@ __global__ __launch_bounds__(SCAN_THREADS) void knn_scan_kernel(ScanParams p) {
     const _Float16* qr = p.q16 + (size_t)(lane_active ? qrow : 0) * DP + h * 8;
 #pragma unroll
     for (int kk = 0; kk < KSTEPS; ++kk) qf[kk] = *(const half8*)(qr + kk * 16);
+    // Retire the fragment loads here, visibly to the compiler: otherwise its waitcnt
+    // scoreboard carries them into the tile loop as `vmcnt(31..0)` waits between the
+    // MFMAs, the last of which drains the next tile's LDS-DMA prefetch.
+#pragma unroll
+    for (int kk = 0; kk < KSTEPS; ++kk) asm volatile("" ::"v"(qf[kk]));
   }
-  float thr = INFINITY;
+  float thr_collect = INFINITY;
   if constexpr (COLLECT) {
-    if (lane_active) thr = p.thresh[qrow];
+    if (lane_active) thr_collect = p.thresh[qrow];
   }
 
   float ls[KL];
@@ -154,6 +213,19 @@ __global__ __launch_bounds__(SCAN_THREADS) void knn_scan_kernel(ScanParams p) {
 
   const int my_tiles = (split < p.ntiles) ? (p.ntiles - 1 - split) / p.splits + 1 : 0;
 
+  // Shared rejection threshold (top-k mode). Every list publishes its KL-th score
+  // (once full) with an agent-scope atomic max; every lane rejects rows scoring <=
+  // the published maximum. Any value ever published is the KL-th of a full list
+  // whose final KL-th can only be larger, so rows rejected this way score <= tau in
+  // K8's certificate and exactness is unaffected; staleness only costs speed. The
+  // value is re-read (sc1, L1 bypass) once per tile and used one tile later, after
+  // the barrier has retired the load, so it never drains the LDS-DMA prefetch.
+  float theta_f = -INFINITY;
+  uint32_t theta_next = 0;
+  float published = -INFINITY;
+  uint32_t* theta_q = nullptr;
+  if constexpr (!COLLECT) theta_q = p.theta + (lane_active ? slot : 0);
+
   // per-lane LDS offsets of the 8 distinct (kk mod 8) A-fragment chunks
   int offA[8];
 #pragma unroll
@@ -161,7 +233,6 @@ __global__ __launch_bounds__(SCAN_THREADS) void knn_scan_kernel(ScanParams p) {
 
   auto stage = [&](int buf, int tile) {
     const char* gt = (const char*)p.x16 + (size_t)tile * TILE_BYTES;
-    char* lt = smem + buf * TILE_BYTES;
 #pragma unroll
     for (int i = 0; i < GLDS_PER_WAVE; ++i) {
       const int piece = w * GLDS_PER_WAVE + i;
@@ -169,34 +240,24 @@ __global__ __launch_bounds__(SCAN_THREADS) void knn_scan_kernel(ScanParams p) {
       const int row = P / CPR;
       const int pos = P - row * CPR;
       const int c = pos ^ (row & 15);
-      __builtin_amdgcn_global_load_lds((const AS1 void*)(gt + row * ROW_BYTES + c * 16),
-                                       (AS3 void*)(lt + piece * 1024), 16, 0, 0);
+      glds_x4(gt + row * ROW_BYTES + c * 16, lds_base + buf * TILE_BYTES + piece * 1024);
     }
-    if (w == 0) {
-      __builtin_amdgcn_global_load_lds((const AS1 void*)(p.labels + (size_t)tile * TILE_ROWS + lane),
-                                       (AS3 void*)(smem + LBL_OFF + buf * TILE_ROWS * 4), 4, 0, 0);
-    }
+    if (w == 0) glds_x1(p.labels + (size_t)tile * TILE_ROWS + lane, lds_base + LBL_OFF + buf * TILE_ROWS * 4);
   };
 
-  auto epilogue = [&](const f32x16& acc, int cur, int rb, int tile) {
-    const int* lbl = (const int*)(smem + LBL_OFF + cur * TILE_ROWS * 4);
-    int4 L[4];
-#pragma unroll
-    for (int g = 0; g < 4; ++g) L[g] = *(const int4*)(lbl + rb + 8 * g + 4 * h);
+  // Slow path: per-row insertion / collection for one 32-row block.
+  auto rows_pass = [&](const f32x16& acc, uint64_t lane_mask, int blk, int tile) {
 #pragma unroll
     for (int reg = 0; reg < 16; ++reg) {
-      const int g = reg >> 2, e = reg & 3;
-      const int lab = e == 0 ? L[g].x : e == 1 ? L[g].y : e == 2 ? L[g].z : L[g].w;
-      const bool ok = (p.label_filter == MRAG_LABEL_ANY) ? (lab >= 0) : (lab == p.label_filter);
-      const float s = ok ? acc[reg] : -INFINITY;
-      const int row = tile * TILE_ROWS + rb + e + 8 * g + 4 * h;
+      const float s = row_ok(lane_mask, blk, reg) ? acc[reg] : -INFINITY;
+      const int row = tile * TILE_ROWS + blk * 32 + 8 * (reg >> 2) + 4 * h + (reg & 3);
       if constexpr (COLLECT) {
-        if (s >= thr) {
+        if (s >= thr_collect) {
           const int pos = atomicAdd(p.cand_cnt + slot, 1);
           if (pos < p.ccap) p.cand[(size_t)slot * p.ccap + pos] = row;
         }
       } else {
-        if (s > ls[KL - 1]) list_insert<KL>(ls, li, s, row);
+        if (s > fmaxf(ls[KL - 1], theta_f)) list_insert<KL>(ls, li, s, row);
       }
     }
   };
@@ -208,10 +269,21 @@ __global__ __launch_bounds__(SCAN_THREADS) void knn_scan_kernel(ScanParams p) {
     for (int it = 0; it < my_tiles; ++it) {
       const int cur = it & 1;
       const int tile = split + it * p.splits;
+      if constexpr (!COLLECT) {
+        if (theta_next != 0) theta_f = fmaxf(theta_f, mrag_ord2f(theta_next));
+        if (wave_active) theta_next = __hip_atomic_load(theta_q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
       if (it + 1 < my_tiles) stage(cur ^ 1, tile + p.splits);
-      if (wave_active) {
-        f32x16 acc0 = {}, acc1 = {};
+
+      // row validity of this tile: one label per lane -> 64-bit ballot (uniform)
+      const int lab = ((const int*)(smem + LBL_OFF + cur * TILE_ROWS * 4))[lane];
+      const bool lab_ok = (p.label_filter == MRAG_LABEL_ANY) ? (lab >= 0) : (lab == p.label_filter);
+      const uint64_t tile_mask = __ballot(lab_ok);
+      const uint64_t lane_mask = tile_mask >> (4 * h);
+
+      if (wave_active && tile_mask != 0) {
         const char* tb = smem + cur * TILE_BYTES;
+        f32x16 acc0 = {}, acc1 = {};
 #pragma unroll
         for (int kk = 0; kk < KSTEPS; ++kk) {
           const int o = offA[kk & 7] + (kk >> 3) * 256;
@@ -220,8 +292,35 @@ __global__ __launch_bounds__(SCAN_THREADS) void knn_scan_kernel(ScanParams p) {
           acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, qf[kk], acc0, 0, 0, 0);
           acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, qf[kk], acc1, 0, 0, 0);
         }
-        epilogue(acc0, cur, 0, tile);
-        epilogue(acc1, cur, 32, tile);
+        if constexpr (ABLATE) {
+          asm volatile("" ::"v"(acc0[0]), "v"(acc0[7]), "v"(acc1[3]), "v"(acc1[15]));
+        } else {
+          float m;
+          if (tile_mask == ~0ull) {
+            m = fmaxf(max16(acc0), max16(acc1));
+          } else {
+            m = fmaxf(masked_max16(acc0, lane_mask, 0), masked_max16(acc1, lane_mask, 1));
+          }
+          float thr;
+          if constexpr (COLLECT) {
+            thr = thr_collect;
+            if (__any(m >= thr)) {
+              rows_pass(acc0, lane_mask, 0, tile);
+              rows_pass(acc1, lane_mask, 1, tile);
+            }
+          } else {
+            thr = fmaxf(ls[KL - 1], theta_f);
+            if (__any(m > thr)) {
+              rows_pass(acc0, lane_mask, 0, tile);
+              rows_pass(acc1, lane_mask, 1, tile);
+              if (li[KL - 1] >= 0 && ls[KL - 1] > published) {
+                published = ls[KL - 1];
+                __hip_atomic_fetch_max(theta_q, mrag_f2ord(published), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+              }
+            }
+          }
+        }
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
@@ -651,11 +750,23 @@ typedef void (*scan_fn)(ScanParams);
 template <int DP>
 scan_fn pick_scan(int KL, bool collect) {
   if (collect) return knn_scan_kernel<DP, 8, true>;
-  // KL = 32 keeps 64 more VGPRs live; at DP >= 384 that spills, so those widths cap at 16
-  // (the certificate stays exact; only the candidate-list depth changes).
-  if (KL <= 8) return knn_scan_kernel<DP, 8, false>;
-  if (KL <= 16 || DP >= 384) return knn_scan_kernel<DP, 16, false>;
-  return knn_scan_kernel<DP, (DP >= 384 ? 16 : 32), false>;
+  // Deeper lists keep 2*KL more VGPRs live next to the DP/4 query-fragment registers;
+  // kl_for() caps KL where it would spill (the certificate stays exact either way).
+  if constexpr (DP >= 512) {
+    return knn_scan_kernel<DP, 8, false>;
+  } else if constexpr (DP >= 256) {
+    return KL <= 8 ? knn_scan_kernel<DP, 8, false> : knn_scan_kernel<DP, 16, false>;
+  } else {
+    return KL <= 8 ? knn_scan_kernel<DP, 8, false>
+                   : (KL <= 16 ? knn_scan_kernel<DP, 16, false> : knn_scan_kernel<DP, 32, false>);
+  }
+}
+
+// Per-lane list depth: >= k where registers allow (DP/4 VGPRs hold the query fragments).
+int kl_for(int k, int DP) {
+  if (k <= 8 || DP >= 512) return 8;
+  if (k <= 16 || DP >= 256) return 16;
+  return 32;
 }
 
 scan_fn get_scan(int DP, int KL, bool collect) {
@@ -685,7 +796,8 @@ struct mrag_knn_index {
   hipStream_t stream = nullptr;
   // search workspace
   DevBuf qin, q32, qn, q16, part_s, part_i, thresh, fail_list, counters, cand_cnt, cand, scratch;
-  DevBuf out_s, out_s64, out_r, stage_rows, stage_labels, rowlist;
+  DevBuf out_s, out_s64, out_r, stage_rows, stage_labels, rowlist, theta;
+  int ablate = 0;  // diagnostic knob, env MRAG_SCAN_ABLATE (timing experiments only)
   int32_t* host_counters = nullptr;  // pinned [2]: fail_cnt, overflow
   int ccap = 4096;
   int64_t last_uncertified = 0, last_retries = 0;
@@ -749,6 +861,7 @@ int mrag_knn_create(int32_t dim, int32_t device, mrag_knn_index** out) {
   ix->device = device;
   ix->D = dim;
   ix->DP = (dim + 127) / 128 * 128;
+  if (const char* ab = getenv("MRAG_SCAN_ABLATE")) ix->ablate = atoi(ab);
   hipError_t e = hipStreamCreateWithFlags(&ix->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipHostMalloc((void**)&ix->host_counters, 16, hipHostMallocDefault);
   if (e != hipSuccess) {
@@ -767,7 +880,7 @@ int mrag_knn_destroy(mrag_knn_index* ix) {
     for (DevBuf* b : {&ix->x16, &ix->x32, &ix->xn, &ix->labels, &ix->qin, &ix->q32, &ix->qn, &ix->q16,
                       &ix->part_s, &ix->part_i, &ix->thresh, &ix->fail_list, &ix->counters,
                       &ix->cand_cnt, &ix->cand, &ix->scratch, &ix->out_s, &ix->out_s64, &ix->out_r,
-                      &ix->stage_rows, &ix->stage_labels, &ix->rowlist})
+                      &ix->stage_rows, &ix->stage_labels, &ix->rowlist, &ix->theta})
       release(*b);
     if (ix->host_counters) (void)hipHostFree(ix->host_counters);
     if (ix->ev0) (void)hipEventDestroy(ix->ev0);
@@ -906,7 +1019,7 @@ int mrag_knn_search(mrag_knn_index* ix, const float* queries, int64_t nq, int32_
     const int64_t Qp = (nq + QPW - 1) / QPW * QPW;
     const int qgroups = (int)((Qp + QPG - 1) / QPG);
     const int ntiles = (int)((ix->n + TILE_ROWS - 1) / TILE_ROWS);
-    const int KL = k <= 8 ? 8 : ((k <= 16 || DP >= 384) ? 16 : 32);
+    const int KL = kl_for(k, DP);
     int S = std::max(1, 256 / qgroups);
     S = std::min(S, ntiles);
     S = std::min(S, MAX_MERGE_ENTRIES / KL);
@@ -930,14 +1043,18 @@ int mrag_knn_search(mrag_knn_index* ix, const float* queries, int64_t nq, int32_
     if (int rc = ensure(ix->fail_list, (size_t)Qp * 4)) return rc;
     if (int rc = ensure(ix->counters, 16)) return rc;
     if (int rc = ensure(ix->cand_cnt, (size_t)Qp * 4)) return rc;
+    if (int rc = ensure(ix->theta, (size_t)Qp * 4)) return rc;
 
     hipLaunchKernelGGL(prep_rows_kernel, dim3((unsigned)((Qp + 3) / 4)), dim3(256), 0, s, qsrc, nq, D, DP,
                        Qp, (float*)ix->q32.p, (double*)ix->qn.p, (_Float16*)ix->q16.p);
     MRAG_CHECK_LAUNCH();
     MRAG_HIP(hipMemsetAsync(ix->counters.p, 0, 16, s));
     MRAG_HIP(hipMemsetAsync(ix->cand_cnt.p, 0, (size_t)Qp * 4, s));
+    MRAG_HIP(hipMemsetAsync(ix->theta.p, 0, (size_t)Qp * 4, s));
 
     ScanParams sp{};
+    sp.theta = (uint32_t*)ix->theta.p;
+
     sp.x16 = (const _Float16*)ix->x16.p;
     sp.labels = (const int32_t*)ix->labels.p;
     sp.q16 = (const _Float16*)ix->q16.p;
@@ -954,6 +1071,7 @@ int mrag_knn_search(mrag_knn_index* ix, const float* queries, int64_t nq, int32_
     sp.cand_cnt = (int32_t*)ix->cand_cnt.p;
 
     scan_fn scan = get_scan(DP, KL, false);
+    if (ix->ablate == 1 && DP == 512) scan = knn_scan_kernel<512, 8, false, true>;  // timing only
     scan_fn collect = get_scan(DP, 8, true);
     if (!scan || !collect) return mrag::fail(MRAG_ERR_UNSUPPORTED, "no scan kernel for DP=%d", DP);
     const dim3 sgrid((unsigned)(qgroups * S));
