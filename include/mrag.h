@@ -119,6 +119,63 @@ int mrag_topk_merge(const double* scores64, const int64_t* rows, int32_t nlists,
                     int32_t k, float* out_scores, double* out_scores64, int64_t* out_rows,
                     void* stream);
 
+/* ---- K1..K5: encoders ----------------------------------------------------
+ * One handle = one encoder tower on one device:
+ *   MRAG_ENC_CLIP_VISION  replaces CLIPModel.get_image_features
+ *                         (app/ml/embeddings.py:84-91, transformers modeling_clip.py:719-755)
+ *   MRAG_ENC_CLIP_TEXT    replaces CLIPModel.get_text_features
+ *                         (app/ml/embeddings.py:101-105, modeling_clip.py:683-717)
+ *   MRAG_ENC_BERT         replaces SentenceTransformer(all-MiniLM-L6-v2).encode =
+ *                         BertModel + mean pooling (app/ml/embeddings.py:62-68)
+ * Parameters are set by Hugging Face state-dict name (f32 host arrays, e.g.
+ * "vision_model.encoder.layers.0.self_attn.q_proj.weight"); compute is fp16 MFMA
+ * GEMMs with f32 accumulation and an f32 residual stream. With normalize != 0 the
+ * output rows go through K6 (the reference's numpy _normalize, bit-exact). */
+#define MRAG_ENC_CLIP_VISION 1
+#define MRAG_ENC_CLIP_TEXT 2
+#define MRAG_ENC_BERT 3
+
+typedef struct mrag_encoder_config {
+  int32_t kind;           /* MRAG_ENC_*                                            */
+  int32_t hidden;         /* 768 (ViT-B/32), 512 (CLIP text), 384 (MiniLM-L6)      */
+  int32_t layers;         /* 12, 12, 6                                             */
+  int32_t heads;          /* 12, 8, 12                                             */
+  int32_t intermediate;   /* 3072, 2048, 1536                                      */
+  int32_t max_positions;  /* text: 77 / 512; vision: unused                        */
+  int32_t vocab;          /* text: 49408 / 30522                                   */
+  int32_t proj_dim;       /* CLIP: 512; BERT: unused                               */
+  int32_t image_size;     /* vision: 224                                           */
+  int32_t patch_size;     /* vision: 32                                            */
+  int32_t act;            /* 0 = quick_gelu (CLIP), 1 = gelu (erf, BERT)          */
+  int32_t eos_token_id;   /* CLIP text pooling: first id == eos (>= 0) or argmax(ids) (-1) */
+  float ln_eps;           /* 1e-5 (CLIP), 1e-12 (BERT)                             */
+} mrag_encoder_config;
+
+typedef struct mrag_encoder mrag_encoder;
+
+int mrag_encoder_create(const mrag_encoder_config* cfg, int32_t device, mrag_encoder** out);
+int mrag_encoder_destroy(mrag_encoder* enc);
+int mrag_encoder_set_param(mrag_encoder* enc, const char* name, const float* data, int64_t numel);
+/* Number of required parameters not set yet (forward fails with MRAG_ERR_STATE until 0). */
+int mrag_encoder_missing(const mrag_encoder* enc, int64_t* count);
+
+/* CLIP image tower: images u8 [batch][S][S][3] (decoded RGB, HWC, S = image_size,
+ * already resized/cropped) -> out f32 [batch][proj_dim]. */
+int mrag_encoder_embed_images(mrag_encoder* enc, const uint8_t* images, int32_t batch, float* out,
+                              int32_t normalize, int32_t ptr_kind, void* stream);
+
+/* Text towers: token ids / attention mask int32 [batch][seq] (mask may be NULL =
+ * all ones) -> out f32 [batch][proj_dim] (CLIP text) or [batch][hidden] (BERT,
+ * mean-pooled over the mask). */
+int mrag_encoder_embed_tokens(mrag_encoder* enc, const int32_t* ids, const int32_t* mask, int32_t batch,
+                              int32_t seq, float* out, int32_t normalize, int32_t ptr_kind, void* stream);
+
+/* K3 building block: C[M][N] (op)= A[M][K] . W[N][K]^T + bias (device pointers;
+ * A, W fp16 row-major; epilogue 0 f16 out, 1 f16 quick_gelu, 2 f16 gelu_erf,
+ * 3 f32 C += , 4 f32 out). N % 128 == 0, K % 64 == 0. */
+int mrag_gemm_nt(const void* A, const void* W, const float* bias, void* C, int32_t M, int32_t N, int32_t K,
+                 int32_t epilogue, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

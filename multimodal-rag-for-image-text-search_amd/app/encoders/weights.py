@@ -1,0 +1,181 @@
+"""Encoder configurations and parameter sources.
+
+The reference loads pretrained weights by hub name (``config.py:10-12``:
+``openai/clip-vit-base-patch32``, ``sentence-transformers/all-MiniLM-L6-v2``) — not
+reachable offline. Parameters therefore come from one of two sources, both keyed by
+the Hugging Face state-dict names the C ABI expects:
+
+* a local checkpoint directory (``model.safetensors``) when ``MODEL_CLIP`` /
+  ``MODEL_TEXT`` points at one (drop-in for real deployments);
+* otherwise a deterministic synthetic generator: a counter-based splitmix64 stream
+  per parameter name, so the GPU box, the oracle and the golden fixtures all see
+  bit-identical weights without shipping 600 MB. Throughput does not depend on the
+  weight values; parity is defined on identical weights (SURVEY.md §7 hard part 2).
+"""
+from __future__ import annotations
+
+import math
+import os
+import zlib
+from dataclasses import dataclass
+from typing import Dict, Iterator, List, Optional, Tuple
+
+import numpy as np
+
+
+@dataclass(frozen=True)
+class EncoderConfig:
+    kind: int  # 1 CLIP vision, 2 CLIP text, 3 BERT
+    hidden: int
+    layers: int
+    heads: int
+    intermediate: int
+    max_positions: int = 0
+    vocab: int = 0
+    proj_dim: int = 0
+    image_size: int = 0
+    patch_size: int = 0
+    act: int = 0  # 0 quick_gelu, 1 gelu_erf
+    eos_token_id: int = -1
+    ln_eps: float = 1e-5
+
+
+# CLIP ViT-B/32 (transformers CLIPVisionConfig defaults == openai/clip-vit-base-patch32)
+CLIP_VISION_B32 = EncoderConfig(kind=1, hidden=768, layers=12, heads=12, intermediate=3072, proj_dim=512,
+                                image_size=224, patch_size=32, act=0, ln_eps=1e-5)
+# CLIP text tower (CLIPTextConfig defaults; eos 49407 -> first-EOS pooling)
+CLIP_TEXT_B32 = EncoderConfig(kind=2, hidden=512, layers=12, heads=8, intermediate=2048, max_positions=77,
+                              vocab=49408, proj_dim=512, act=0, eos_token_id=49407, ln_eps=1e-5)
+# all-MiniLM-L6-v2 = BertModel(hidden 384, 6 layers, 12 heads, intermediate 1536)
+MINILM_L6 = EncoderConfig(kind=3, hidden=384, layers=6, heads=12, intermediate=1536, max_positions=512,
+                          vocab=30522, act=1, ln_eps=1e-12)
+
+
+def param_specs(cfg: EncoderConfig) -> List[Tuple[str, Tuple[int, ...], str]]:
+    """(state-dict name, shape, init kind) of every parameter the forward reads."""
+    D, I = cfg.hidden, cfg.intermediate
+    out: List[Tuple[str, Tuple[int, ...], str]] = []
+    if cfg.kind in (1, 2):
+        pre = "vision_model." if cfg.kind == 1 else "text_model."
+        if cfg.kind == 1:
+            g = cfg.image_size // cfg.patch_size
+            out += [
+                (pre + "embeddings.class_embedding", (D,), "emb"),
+                (pre + "embeddings.patch_embedding.weight", (D, 3, cfg.patch_size, cfg.patch_size), "linear"),
+                (pre + "embeddings.position_embedding.weight", (g * g + 1, D), "emb"),
+                (pre + "pre_layrnorm.weight", (D,), "ln_w"),
+                (pre + "pre_layrnorm.bias", (D,), "ln_b"),
+            ]
+        else:
+            out += [
+                (pre + "embeddings.token_embedding.weight", (cfg.vocab, D), "emb"),
+                (pre + "embeddings.position_embedding.weight", (cfg.max_positions, D), "emb"),
+            ]
+        for i in range(cfg.layers):
+            l = f"{pre}encoder.layers.{i}."
+            for p in ("q_proj", "k_proj", "v_proj", "out_proj"):
+                out += [(l + f"self_attn.{p}.weight", (D, D), "linear"), (l + f"self_attn.{p}.bias", (D,), "bias")]
+            out += [
+                (l + "layer_norm1.weight", (D,), "ln_w"), (l + "layer_norm1.bias", (D,), "ln_b"),
+                (l + "layer_norm2.weight", (D,), "ln_w"), (l + "layer_norm2.bias", (D,), "ln_b"),
+                (l + "mlp.fc1.weight", (I, D), "linear"), (l + "mlp.fc1.bias", (I,), "bias"),
+                (l + "mlp.fc2.weight", (D, I), "linear"), (l + "mlp.fc2.bias", (D,), "bias"),
+            ]
+        if cfg.kind == 1:
+            out += [
+                (pre + "post_layernorm.weight", (D,), "ln_w"), (pre + "post_layernorm.bias", (D,), "ln_b"),
+                ("visual_projection.weight", (cfg.proj_dim, D), "linear"),
+            ]
+        else:
+            out += [
+                (pre + "final_layer_norm.weight", (D,), "ln_w"), (pre + "final_layer_norm.bias", (D,), "ln_b"),
+                ("text_projection.weight", (cfg.proj_dim, D), "linear"),
+            ]
+    else:
+        out += [
+            ("embeddings.word_embeddings.weight", (cfg.vocab, D), "emb"),
+            ("embeddings.position_embeddings.weight", (cfg.max_positions, D), "emb"),
+            ("embeddings.token_type_embeddings.weight", (2, D), "emb"),
+            ("embeddings.LayerNorm.weight", (D,), "ln_w"),
+            ("embeddings.LayerNorm.bias", (D,), "ln_b"),
+        ]
+        for i in range(cfg.layers):
+            l = f"encoder.layer.{i}."
+            for p in ("query", "key", "value"):
+                out += [(l + f"attention.self.{p}.weight", (D, D), "linear"), (l + f"attention.self.{p}.bias", (D,), "bias")]
+            out += [
+                (l + "attention.output.dense.weight", (D, D), "linear"), (l + "attention.output.dense.bias", (D,), "bias"),
+                (l + "attention.output.LayerNorm.weight", (D,), "ln_w"), (l + "attention.output.LayerNorm.bias", (D,), "ln_b"),
+                (l + "intermediate.dense.weight", (I, D), "linear"), (l + "intermediate.dense.bias", (I,), "bias"),
+                (l + "output.dense.weight", (D, I), "linear"), (l + "output.dense.bias", (D,), "bias"),
+                (l + "output.LayerNorm.weight", (D,), "ln_w"), (l + "output.LayerNorm.bias", (D,), "ln_b"),
+            ]
+    return out
+
+
+_M64 = np.uint64(0xFFFFFFFFFFFFFFFF)
+
+
+def _splitmix64(x: np.ndarray) -> np.ndarray:
+    with np.errstate(over="ignore"):
+        z = x + np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return z ^ (z >> np.uint64(31))
+
+
+def _uniform(name: str, n: int, seed: int) -> np.ndarray:
+    """n values in [-1, 1) from a counter-based stream keyed by (name, seed)."""
+    key = np.uint64((zlib.crc32(name.encode()) << 32) | (zlib.adler32(name.encode()) & 0xFFFFFFFF)) ^ np.uint64(seed)
+    ctr = np.arange(n, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        z = _splitmix64(ctr * np.uint64(0xD1B54A32D192ED03) + key)
+    u = (z >> np.uint64(11)).astype(np.float64) * (1.0 / 9007199254740992.0)
+    return (2.0 * u - 1.0).astype(np.float32)
+
+
+def synth_param(name: str, shape: Tuple[int, ...], kind: str, seed: int = 0) -> np.ndarray:
+    n = int(np.prod(shape))
+    u = _uniform(name, n, seed)
+    if kind == "linear":
+        fan_in = int(np.prod(shape[1:]))
+        v = u * np.float32(math.sqrt(3.0 / fan_in))
+    elif kind == "bias":
+        v = u * np.float32(0.02)
+    elif kind == "ln_w":
+        v = np.float32(1.0) + u * np.float32(0.1)
+    elif kind == "ln_b":
+        v = u * np.float32(0.05)
+    elif kind == "emb":
+        v = u * np.float32(0.1)
+    else:
+        raise ValueError(kind)
+    return v.reshape(shape).astype(np.float32)
+
+
+def synth_state_dict(cfg: EncoderConfig, seed: int = 0) -> Iterator[Tuple[str, np.ndarray]]:
+    for name, shape, kind in param_specs(cfg):
+        yield name, synth_param(name, shape, kind, seed)
+
+
+def checkpoint_state_dict(path: str, cfg: EncoderConfig) -> Optional[Dict[str, np.ndarray]]:
+    """Read a local Hugging Face checkpoint (safetensors) if `path` is a directory
+    holding one; None otherwise. Only the names param_specs() lists are returned."""
+    if not path or not os.path.isdir(path):
+        return None
+    files = [f for f in os.listdir(path) if f.endswith(".safetensors")]
+    if not files:
+        return None
+    from safetensors.numpy import load_file
+
+    want = {n for n, _, _ in param_specs(cfg)}
+    out: Dict[str, np.ndarray] = {}
+    for f in sorted(files):
+        for k, v in load_file(os.path.join(path, f)).items():
+            for cand in (k, k.replace("0.auto_model.", ""), k.replace("bert.", "")):
+                if cand in want:
+                    out[cand] = np.asarray(v, dtype=np.float32)
+    missing = want - set(out)
+    if missing:
+        raise ValueError(f"checkpoint {path} lacks {len(missing)} parameters, e.g. {sorted(missing)[:3]}")
+    return out

@@ -1,0 +1,581 @@
+// encoder.hip — native runner of the three encoders behind include/mrag.h:
+//   MRAG_ENC_CLIP_VISION  CLIPModel.get_image_features  (app/ml/embeddings.py:84-91)
+//   MRAG_ENC_CLIP_TEXT    CLIPModel.get_text_features   (app/ml/embeddings.py:101-105)
+//   MRAG_ENC_BERT         SentenceTransformer(all-MiniLM-L6-v2).encode: BERT + mean pool
+//                         (app/ml/embeddings.py:62-70)
+// Parameters arrive under their Hugging Face state-dict names (f32 host arrays) and are
+// packed once into device buffers: f16 GEMM weights with q|k|v fused into one [3D][D]
+// matrix, f32 biases / LayerNorm params / embeddings. A forward is ~7 launches per layer
+// on one HIP stream; activations live in a per-handle workspace sized for the largest
+// batch seen.
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "common.h"
+#include "encoder_kernels.h"
+
+using namespace mrag_enc;
+
+namespace {
+
+struct Buf {
+  void* p = nullptr;
+  size_t bytes = 0;
+};
+
+int buf_ensure(Buf& b, size_t bytes) {
+  if (b.p && b.bytes >= bytes) return MRAG_OK;
+  if (b.p) MRAG_HIP(hipFree(b.p));
+  b.p = nullptr;
+  b.bytes = 0;
+  MRAG_HIP(hipMalloc(&b.p, std::max<size_t>(bytes, 256)));
+  b.bytes = std::max<size_t>(bytes, 256);
+  return MRAG_OK;
+}
+
+void buf_free(Buf& b) {
+  if (b.p) (void)hipFree(b.p);
+  b.p = nullptr;
+  b.bytes = 0;
+}
+
+struct Layer {
+  Buf wqkv, bqkv, wo, bo, w1, b1, w2, b2, ln1g, ln1b, ln2g, ln2b;
+};
+
+__global__ void f32_to_f16_kernel(const float* __restrict__ in, _Float16* __restrict__ out, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = (_Float16)in[i];
+}
+
+}  // namespace
+
+struct mrag_encoder {
+  std::mutex mu;
+  mrag_encoder_config cfg;
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::vector<Layer> layers;
+  // embeddings / heads
+  Buf patch_w, cls, pos, pre_g, pre_b, post_g, post_b, proj_w;  // vision
+  Buf tok, type0, emb_g, emb_b;                                  // text / bert (+pos)
+  std::map<std::string, bool> loaded;
+  std::vector<std::string> expected;
+  // workspace
+  Buf X, H16, QKV, ATT, F16, PATCH, IMG, IDS, MASK, ROWS, POOL16, OUT;
+  int64_t ws_tokens = 0;
+};
+
+namespace {
+
+// Upload n floats from host to a device buffer as f32 or f16.
+int upload(Buf& b, const float* host, int64_t n, bool to_f16, hipStream_t s) {
+  if (!to_f16) {
+    if (int rc = buf_ensure(b, (size_t)n * 4)) return rc;
+    MRAG_HIP(hipMemcpyAsync(b.p, host, (size_t)n * 4, hipMemcpyHostToDevice, s));
+    return MRAG_OK;
+  }
+  if (int rc = buf_ensure(b, (size_t)n * 2)) return rc;
+  void* tmp = nullptr;
+  MRAG_HIP(hipMalloc(&tmp, (size_t)n * 4));
+  hipError_t e = hipMemcpyAsync(tmp, host, (size_t)n * 4, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(f32_to_f16_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, (const float*)tmp,
+                       (_Float16*)b.p, n);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  (void)hipFree(tmp);
+  if (e != hipSuccess) return mrag::fail(MRAG_ERR_HIP, "upload: %s", hipGetErrorString(e));
+  return MRAG_OK;
+}
+
+// Copy into a slice [off, off+n) of an f16 buffer of `total` elements (fused QKV).
+int upload_slice_f16(Buf& b, int64_t total, int64_t off, const float* host, int64_t n, hipStream_t s) {
+  if (!b.p) {
+    if (int rc = buf_ensure(b, (size_t)total * 2)) return rc;
+  }
+  void* tmp = nullptr;
+  MRAG_HIP(hipMalloc(&tmp, (size_t)n * 4));
+  hipError_t e = hipMemcpyAsync(tmp, host, (size_t)n * 4, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(f32_to_f16_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, (const float*)tmp,
+                       (_Float16*)b.p + off, n);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  (void)hipFree(tmp);
+  if (e != hipSuccess) return mrag::fail(MRAG_ERR_HIP, "upload: %s", hipGetErrorString(e));
+  return MRAG_OK;
+}
+
+int upload_slice_f32(Buf& b, int64_t total, int64_t off, const float* host, int64_t n, hipStream_t s) {
+  if (!b.p) {
+    if (int rc = buf_ensure(b, (size_t)total * 4)) return rc;
+  }
+  MRAG_HIP(hipMemcpyAsync((float*)b.p + off, host, (size_t)n * 4, hipMemcpyHostToDevice, s));
+  MRAG_HIP(hipStreamSynchronize(s));
+  return MRAG_OK;
+}
+
+bool starts_with(const std::string& s, const std::string& p) { return s.compare(0, p.size(), p) == 0; }
+
+// Expected state-dict names for a config (everything the forward reads).
+std::vector<std::string> expected_names(const mrag_encoder_config& c) {
+  std::vector<std::string> v;
+  if (c.kind == MRAG_ENC_CLIP_VISION || c.kind == MRAG_ENC_CLIP_TEXT) {
+    const std::string pre = c.kind == MRAG_ENC_CLIP_VISION ? "vision_model." : "text_model.";
+    if (c.kind == MRAG_ENC_CLIP_VISION) {
+      for (const char* n : {"embeddings.class_embedding", "embeddings.patch_embedding.weight",
+                            "embeddings.position_embedding.weight", "pre_layrnorm.weight", "pre_layrnorm.bias",
+                            "post_layernorm.weight", "post_layernorm.bias"})
+        v.push_back(pre + n);
+      v.push_back("visual_projection.weight");
+    } else {
+      for (const char* n : {"embeddings.token_embedding.weight", "embeddings.position_embedding.weight",
+                            "final_layer_norm.weight", "final_layer_norm.bias"})
+        v.push_back(pre + n);
+      v.push_back("text_projection.weight");
+    }
+    for (int i = 0; i < c.layers; ++i) {
+      const std::string l = pre + "encoder.layers." + std::to_string(i) + ".";
+      for (const char* n : {"self_attn.q_proj.weight", "self_attn.q_proj.bias", "self_attn.k_proj.weight",
+                            "self_attn.k_proj.bias", "self_attn.v_proj.weight", "self_attn.v_proj.bias",
+                            "self_attn.out_proj.weight", "self_attn.out_proj.bias", "layer_norm1.weight",
+                            "layer_norm1.bias", "layer_norm2.weight", "layer_norm2.bias", "mlp.fc1.weight",
+                            "mlp.fc1.bias", "mlp.fc2.weight", "mlp.fc2.bias"})
+        v.push_back(l + n);
+    }
+  } else {
+    for (const char* n : {"embeddings.word_embeddings.weight", "embeddings.position_embeddings.weight",
+                          "embeddings.token_type_embeddings.weight", "embeddings.LayerNorm.weight",
+                          "embeddings.LayerNorm.bias"})
+      v.push_back(n);
+    for (int i = 0; i < c.layers; ++i) {
+      const std::string l = "encoder.layer." + std::to_string(i) + ".";
+      for (const char* n : {"attention.self.query.weight", "attention.self.query.bias", "attention.self.key.weight",
+                            "attention.self.key.bias", "attention.self.value.weight", "attention.self.value.bias",
+                            "attention.output.dense.weight", "attention.output.dense.bias",
+                            "attention.output.LayerNorm.weight", "attention.output.LayerNorm.bias",
+                            "intermediate.dense.weight", "intermediate.dense.bias", "output.dense.weight",
+                            "output.dense.bias", "output.LayerNorm.weight", "output.LayerNorm.bias"})
+        v.push_back(l + n);
+    }
+  }
+  return v;
+}
+
+int64_t expected_numel(const mrag_encoder_config& c, const std::string& name) {
+  const int64_t D = c.hidden, I = c.intermediate;
+  auto ends = [&](const char* suf) {
+    const size_t n = strlen(suf);
+    return name.size() >= n && name.compare(name.size() - n, n, suf) == 0;
+  };
+  if (ends("class_embedding")) return D;
+  if (ends("patch_embedding.weight")) return D * 3 * c.patch_size * c.patch_size;
+  if (ends("embeddings.position_embedding.weight") || ends("position_embeddings.weight")) {
+    if (c.kind == MRAG_ENC_CLIP_VISION) {
+      const int64_t g = c.image_size / c.patch_size;
+      return (g * g + 1) * D;
+    }
+    return (int64_t)c.max_positions * D;
+  }
+  if (ends("token_embedding.weight") || ends("word_embeddings.weight")) return (int64_t)c.vocab * D;
+  if (ends("token_type_embeddings.weight")) return 2 * D;
+  if (ends("visual_projection.weight") || ends("text_projection.weight")) return (int64_t)c.proj_dim * D;
+  if (ends("fc1.weight") || ends("intermediate.dense.weight")) return I * D;
+  if (ends("fc1.bias") || ends("intermediate.dense.bias")) return I;
+  if (ends("fc2.weight") || (ends("output.dense.weight") && name.find("attention") == std::string::npos)) return D * I;
+  if (ends(".weight") && (name.find("proj.weight") != std::string::npos || name.find("self.query") != std::string::npos ||
+                          name.find("self.key") != std::string::npos || name.find("self.value") != std::string::npos ||
+                          name.find("attention.output.dense") != std::string::npos))
+    return D * D;
+  return D;  // biases, LayerNorm params
+}
+
+int layer_index(const std::string& name, const std::string& marker) {
+  const size_t p = name.find(marker);
+  if (p == std::string::npos) return -1;
+  return atoi(name.c_str() + p + marker.size());
+}
+
+int ensure_workspace(mrag_encoder* e, int B, int T) {
+  const int64_t tokens = (int64_t)B * T;
+  if (tokens <= e->ws_tokens) return MRAG_OK;
+  const auto& c = e->cfg;
+  const int64_t D = c.hidden, I = c.intermediate;
+  if (int rc = buf_ensure(e->X, tokens * D * 4)) return rc;
+  if (int rc = buf_ensure(e->H16, tokens * D * 2)) return rc;
+  if (int rc = buf_ensure(e->QKV, tokens * 3 * D * 2)) return rc;
+  if (int rc = buf_ensure(e->ATT, tokens * D * 2)) return rc;
+  int64_t f16n = tokens * I;
+  if (c.kind == MRAG_ENC_CLIP_VISION) f16n = std::max<int64_t>(f16n, tokens * 3 * c.patch_size * c.patch_size);
+  if (int rc = buf_ensure(e->F16, f16n * 2)) return rc;
+  if (c.kind == MRAG_ENC_CLIP_VISION) {
+    if (int rc = buf_ensure(e->PATCH, tokens * D * 4)) return rc;
+  }
+  if (int rc = buf_ensure(e->ROWS, (size_t)B * 4 + 256)) return rc;
+  if (int rc = buf_ensure(e->POOL16, (size_t)B * D * 2)) return rc;
+  e->ws_tokens = tokens;
+  return MRAG_OK;
+}
+
+// GEMM helper: C = A[M][K] . W[N][K]^T (+bias), epilogue
+int gemm(const void* A, const void* W, const void* bias, void* C, int M, int N, int K, int ldc, int epi,
+         hipStream_t s) {
+  GemmArgs g{};
+  g.A = (const _Float16*)A;
+  g.W = (const _Float16*)W;
+  g.bias = (const float*)bias;
+  g.C = C;
+  g.M = M;
+  g.N = N;
+  g.K = K;
+  g.lda = K;
+  g.ldw = K;
+  g.ldc = ldc;
+  return launch_gemm(g, epi, s);
+}
+
+int layernorm(const float* x, const int* gather, float* y32, _Float16* y16, const Buf& g, const Buf& b, int rows,
+              int D, float eps, hipStream_t s) {
+  LayerNormArgs a{};
+  a.x = x;
+  a.gather = gather;
+  a.y32 = y32;
+  a.y16 = y16;
+  a.gamma = (const float*)g.p;
+  a.beta = (const float*)b.p;
+  a.rows = rows;
+  a.D = D;
+  a.ldx = D;
+  a.eps = eps;
+  return launch_layernorm(a, s);
+}
+
+// Pre-LN transformer layer (CLIP): X += attn(LN1(X)); X += mlp(LN2(X)).
+int clip_layer(mrag_encoder* e, const Layer& L, int B, int T, const int32_t* mask, int causal, hipStream_t s) {
+  const auto& c = e->cfg;
+  const int D = c.hidden, I = c.intermediate, M = B * T;
+  float* X = (float*)e->X.p;
+  _Float16* H = (_Float16*)e->H16.p;
+  if (int rc = layernorm(X, nullptr, nullptr, H, L.ln1g, L.ln1b, M, D, c.ln_eps, s)) return rc;
+  if (int rc = gemm(H, L.wqkv.p, L.bqkv.p, e->QKV.p, M, 3 * D, D, 3 * D, EPI_F16, s)) return rc;
+  AttentionArgs a{};
+  a.qkv = (const _Float16*)e->QKV.p;
+  a.out = (_Float16*)e->ATT.p;
+  a.mask = mask;
+  a.B = B;
+  a.L = T;
+  a.H = c.heads;
+  a.causal = causal;
+  a.scale = 1.0f / sqrtf((float)(D / c.heads));
+  if (int rc = launch_attention(a, D / c.heads, s)) return rc;
+  if (int rc = gemm(e->ATT.p, L.wo.p, L.bo.p, X, M, D, D, D, EPI_F32_RESIDUAL, s)) return rc;
+  if (int rc = layernorm(X, nullptr, nullptr, H, L.ln2g, L.ln2b, M, D, c.ln_eps, s)) return rc;
+  const int act = c.act == 0 ? EPI_F16_QUICK_GELU : EPI_F16_GELU_ERF;
+  if (int rc = gemm(H, L.w1.p, L.b1.p, e->F16.p, M, I, D, I, act, s)) return rc;
+  return gemm(e->F16.p, L.w2.p, L.b2.p, X, M, D, I, D, EPI_F32_RESIDUAL, s);
+}
+
+// Post-LN transformer layer (BERT): X = LN(X + attn(X)); X = LN(X + ffn(X)).
+// Invariant on entry and exit: X (f32) and H16 == f16(X).
+int bert_layer(mrag_encoder* e, const Layer& L, int B, int T, const int32_t* mask, hipStream_t s) {
+  const auto& c = e->cfg;
+  const int D = c.hidden, I = c.intermediate, M = B * T;
+  float* X = (float*)e->X.p;
+  _Float16* H = (_Float16*)e->H16.p;
+  if (int rc = gemm(H, L.wqkv.p, L.bqkv.p, e->QKV.p, M, 3 * D, D, 3 * D, EPI_F16, s)) return rc;
+  AttentionArgs a{};
+  a.qkv = (const _Float16*)e->QKV.p;
+  a.out = (_Float16*)e->ATT.p;
+  a.mask = mask;
+  a.B = B;
+  a.L = T;
+  a.H = c.heads;
+  a.causal = 0;
+  a.scale = 1.0f / sqrtf((float)(D / c.heads));
+  if (int rc = launch_attention(a, D / c.heads, s)) return rc;
+  if (int rc = gemm(e->ATT.p, L.wo.p, L.bo.p, X, M, D, D, D, EPI_F32_RESIDUAL, s)) return rc;
+  if (int rc = layernorm(X, nullptr, X, H, L.ln1g, L.ln1b, M, D, c.ln_eps, s)) return rc;
+  if (int rc = gemm(H, L.w1.p, L.b1.p, e->F16.p, M, I, D, I, EPI_F16_GELU_ERF, s)) return rc;
+  if (int rc = gemm(e->F16.p, L.w2.p, L.b2.p, X, M, D, I, D, EPI_F32_RESIDUAL, s)) return rc;
+  return layernorm(X, nullptr, X, H, L.ln2g, L.ln2b, M, D, c.ln_eps, s);
+}
+
+int check_ready(mrag_encoder* e) {
+  for (const auto& n : e->expected)
+    if (!e->loaded.count(n)) return mrag::fail(MRAG_ERR_STATE, "encoder parameter '%s' not set", n.c_str());
+  return MRAG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mrag_encoder_create(const mrag_encoder_config* cfg, int32_t device, mrag_encoder** out) {
+  MRAG_REQUIRE(cfg && out, "NULL argument");
+  *out = nullptr;
+  const auto& c = *cfg;
+  MRAG_REQUIRE(c.kind == MRAG_ENC_CLIP_VISION || c.kind == MRAG_ENC_CLIP_TEXT || c.kind == MRAG_ENC_BERT,
+               "unknown encoder kind %d", c.kind);
+  MRAG_REQUIRE(c.hidden > 0 && c.hidden % 128 == 0 && c.hidden <= 1024, "hidden %d unsupported (multiple of 128, <= 1024)",
+               c.hidden);
+  MRAG_REQUIRE(c.intermediate % 128 == 0 && c.intermediate > 0, "intermediate %d must be a multiple of 128",
+               c.intermediate);
+  MRAG_REQUIRE(c.heads > 0 && c.hidden % c.heads == 0 && (c.hidden / c.heads == 64 || c.hidden / c.heads == 32),
+               "head_dim must be 32 or 64");
+  MRAG_REQUIRE(c.layers >= 1 && c.layers <= 64, "layers %d", c.layers);
+  MRAG_REQUIRE(c.act == 0 || c.act == 1, "act %d", c.act);
+  if (c.kind != MRAG_ENC_BERT) MRAG_REQUIRE(c.proj_dim % 128 == 0 && c.proj_dim > 0, "proj_dim must be a multiple of 128");
+  if (c.kind == MRAG_ENC_CLIP_VISION)
+    MRAG_REQUIRE(c.patch_size > 0 && c.image_size % c.patch_size == 0 && (3 * c.patch_size * c.patch_size) % 64 == 0 &&
+                     c.patch_size % 8 == 0,
+                 "image/patch size unsupported");
+  int ndev = 0;
+  MRAG_HIP(hipGetDeviceCount(&ndev));
+  MRAG_REQUIRE(device >= 0 && device < ndev, "device %d out of range", device);
+  mrag::DeviceGuard g(device);
+  auto* e = new mrag_encoder();
+  e->cfg = c;
+  e->device = device;
+  e->layers.resize(c.layers);
+  e->expected = expected_names(c);
+  hipError_t err = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
+  if (err != hipSuccess) {
+    delete e;
+    return mrag::fail(MRAG_ERR_HIP, "stream: %s", hipGetErrorString(err));
+  }
+  *out = e;
+  return MRAG_OK;
+}
+
+int mrag_encoder_destroy(mrag_encoder* e) {
+  if (!e) return MRAG_OK;
+  {
+    mrag::DeviceGuard g(e->device);
+    (void)hipStreamSynchronize(e->stream);
+    for (auto& L : e->layers)
+      for (Buf* b : {&L.wqkv, &L.bqkv, &L.wo, &L.bo, &L.w1, &L.b1, &L.w2, &L.b2, &L.ln1g, &L.ln1b, &L.ln2g, &L.ln2b})
+        buf_free(*b);
+    for (Buf* b : {&e->patch_w, &e->cls, &e->pos, &e->pre_g, &e->pre_b, &e->post_g, &e->post_b, &e->proj_w, &e->tok,
+                   &e->type0, &e->emb_g, &e->emb_b, &e->X, &e->H16, &e->QKV, &e->ATT, &e->F16, &e->PATCH, &e->IMG,
+                   &e->IDS, &e->MASK, &e->ROWS, &e->POOL16, &e->OUT})
+      buf_free(*b);
+    (void)hipStreamDestroy(e->stream);
+  }
+  delete e;
+  return MRAG_OK;
+}
+
+int mrag_encoder_set_param(mrag_encoder* e, const char* cname, const float* data, int64_t numel) {
+  MRAG_REQUIRE(e && cname && data, "NULL argument");
+  std::lock_guard<std::mutex> lk(e->mu);
+  mrag::DeviceGuard g(e->device);
+  const std::string name(cname);
+  const auto& c = e->cfg;
+  bool known = false;
+  for (const auto& n : e->expected)
+    if (n == name) known = true;
+  MRAG_REQUIRE(known, "unexpected parameter '%s' for this encoder", cname);
+  const int64_t want = expected_numel(c, name);
+  MRAG_REQUIRE(numel == want, "parameter '%s': %lld elements, expected %lld", cname, (long long)numel, (long long)want);
+  hipStream_t s = e->stream;
+  const int64_t D = c.hidden;
+  auto ends = [&](const char* suf) {
+    const size_t n = strlen(suf);
+    return name.size() >= n && name.compare(name.size() - n, n, suf) == 0;
+  };
+  int rc = MRAG_OK;
+  const int li = c.kind == MRAG_ENC_BERT ? layer_index(name, "encoder.layer.") : layer_index(name, "encoder.layers.");
+  if (li >= 0) {
+    MRAG_REQUIRE(li < c.layers, "layer index %d out of range", li);
+    Layer& L = e->layers[li];
+    int qkv = -1;
+    bool is_w = ends(".weight");
+    if (name.find("q_proj") != std::string::npos || name.find("self.query") != std::string::npos) qkv = 0;
+    if (name.find("k_proj") != std::string::npos || name.find("self.key") != std::string::npos) qkv = 1;
+    if (name.find("v_proj") != std::string::npos || name.find("self.value") != std::string::npos) qkv = 2;
+    if (qkv >= 0) {
+      rc = is_w ? upload_slice_f16(L.wqkv, 3 * D * D, qkv * D * D, data, numel, s)
+                : upload_slice_f32(L.bqkv, 3 * D, qkv * D, data, numel, s);
+    } else if (name.find("out_proj") != std::string::npos || name.find("attention.output.dense") != std::string::npos) {
+      rc = is_w ? upload(L.wo, data, numel, true, s) : upload(L.bo, data, numel, false, s);
+    } else if (name.find("fc1") != std::string::npos || name.find("intermediate.dense") != std::string::npos) {
+      rc = is_w ? upload(L.w1, data, numel, true, s) : upload(L.b1, data, numel, false, s);
+    } else if (name.find("fc2") != std::string::npos || name.find("output.dense") != std::string::npos) {
+      rc = is_w ? upload(L.w2, data, numel, true, s) : upload(L.b2, data, numel, false, s);
+    } else if (name.find("layer_norm1") != std::string::npos ||
+               name.find("attention.output.LayerNorm") != std::string::npos) {
+      rc = is_w ? upload(L.ln1g, data, numel, false, s) : upload(L.ln1b, data, numel, false, s);
+    } else if (name.find("layer_norm2") != std::string::npos || name.find("output.LayerNorm") != std::string::npos) {
+      rc = is_w ? upload(L.ln2g, data, numel, false, s) : upload(L.ln2b, data, numel, false, s);
+    } else {
+      return mrag::fail(MRAG_ERR_ARG, "unhandled layer parameter '%s'", cname);
+    }
+  } else if (ends("class_embedding")) {
+    rc = upload(e->cls, data, numel, false, s);
+  } else if (ends("patch_embedding.weight")) {
+    rc = upload(e->patch_w, data, numel, true, s);  // [D][3][P][P] == [D][K] row-major
+  } else if (ends("position_embedding.weight") || ends("position_embeddings.weight")) {
+    rc = upload(e->pos, data, numel, false, s);
+  } else if (ends("token_embedding.weight") || ends("word_embeddings.weight")) {
+    rc = upload(e->tok, data, numel, false, s);
+  } else if (ends("token_type_embeddings.weight")) {
+    rc = upload(e->type0, data, D, false, s);  // row 0 only (token_type_ids == 0)
+  } else if (ends("pre_layrnorm.weight")) {
+    rc = upload(e->pre_g, data, numel, false, s);
+  } else if (ends("pre_layrnorm.bias")) {
+    rc = upload(e->pre_b, data, numel, false, s);
+  } else if (ends("post_layernorm.weight") || ends("final_layer_norm.weight")) {
+    rc = upload(e->post_g, data, numel, false, s);
+  } else if (ends("post_layernorm.bias") || ends("final_layer_norm.bias")) {
+    rc = upload(e->post_b, data, numel, false, s);
+  } else if (ends("embeddings.LayerNorm.weight")) {
+    rc = upload(e->emb_g, data, numel, false, s);
+  } else if (ends("embeddings.LayerNorm.bias")) {
+    rc = upload(e->emb_b, data, numel, false, s);
+  } else if (ends("visual_projection.weight") || ends("text_projection.weight")) {
+    rc = upload(e->proj_w, data, numel, true, s);
+  } else {
+    return mrag::fail(MRAG_ERR_ARG, "unhandled parameter '%s'", cname);
+  }
+  if (rc) return rc;
+  MRAG_HIP(hipStreamSynchronize(s));
+  e->loaded[name] = true;
+  return MRAG_OK;
+}
+
+int mrag_encoder_missing(const mrag_encoder* e, int64_t* count) {
+  MRAG_REQUIRE(e && count, "NULL argument");
+  int64_t n = 0;
+  for (const auto& name : e->expected)
+    if (!e->loaded.count(name)) ++n;
+  *count = n;
+  return MRAG_OK;
+}
+
+int mrag_encoder_embed_images(mrag_encoder* e, const uint8_t* images, int32_t batch, float* out, int32_t normalize,
+                              int32_t ptr_kind, void* stream_arg) {
+  MRAG_REQUIRE(e != nullptr, "NULL encoder");
+  MRAG_REQUIRE(e->cfg.kind == MRAG_ENC_CLIP_VISION, "not an image encoder");
+  MRAG_REQUIRE(batch >= 0, "negative batch");
+  MRAG_REQUIRE(ptr_kind == MRAG_PTR_HOST || ptr_kind == MRAG_PTR_DEVICE, "bad ptr_kind");
+  std::lock_guard<std::mutex> lk(e->mu);
+  mrag::DeviceGuard g(e->device);
+  if (int rc = check_ready(e)) return rc;
+  if (batch == 0) return MRAG_OK;
+  MRAG_REQUIRE(images && out, "NULL images/out");
+  hipStream_t s = stream_arg ? (hipStream_t)stream_arg : e->stream;
+  const auto& c = e->cfg;
+  const int S = c.image_size, P = c.patch_size, G = S / P, T = G * G + 1, D = c.hidden, B = batch;
+  const int Kp = 3 * P * P;
+  if (int rc = ensure_workspace(e, B, T)) return rc;
+  const uint8_t* img = images;
+  if (ptr_kind == MRAG_PTR_HOST) {
+    if (int rc = buf_ensure(e->IMG, (size_t)B * S * S * 3)) return rc;
+    MRAG_HIP(hipMemcpyAsync(e->IMG.p, images, (size_t)B * S * S * 3, hipMemcpyHostToDevice, s));
+    img = (const uint8_t*)e->IMG.p;
+  }
+  float* X = (float*)e->X.p;
+  if (int rc = launch_vit_im2col(img, (_Float16*)e->F16.p, B, S, P, s)) return rc;
+  if (int rc = gemm(e->F16.p, e->patch_w.p, nullptr, e->PATCH.p, B * (T - 1), D, Kp, D, EPI_F32, s)) return rc;
+  if (int rc = launch_vit_assemble((const float*)e->PATCH.p, (const float*)e->cls.p, (const float*)e->pos.p, X, B, T,
+                                   D, s))
+    return rc;
+  if (int rc = layernorm(X, nullptr, X, nullptr, e->pre_g, e->pre_b, B * T, D, c.ln_eps, s)) return rc;
+  for (int i = 0; i < c.layers; ++i)
+    if (int rc = clip_layer(e, e->layers[i], B, T, nullptr, 0, s)) return rc;
+  if (int rc = launch_cls_rows(B, T, (int*)e->ROWS.p, s)) return rc;
+  if (int rc = layernorm(X, (const int*)e->ROWS.p, nullptr, (_Float16*)e->POOL16.p, e->post_g, e->post_b, B, D,
+                         c.ln_eps, s))
+    return rc;
+  float* dst = out;
+  if (ptr_kind == MRAG_PTR_HOST) {
+    if (int rc = buf_ensure(e->OUT, (size_t)B * c.proj_dim * 4)) return rc;
+    dst = (float*)e->OUT.p;
+  }
+  if (int rc = gemm(e->POOL16.p, e->proj_w.p, nullptr, dst, B, c.proj_dim, D, c.proj_dim, EPI_F32, s)) return rc;
+  if (normalize)
+    if (int rc = mrag_l2norm_rows(dst, dst, B, c.proj_dim, s)) return rc;
+  if (ptr_kind == MRAG_PTR_HOST)
+    MRAG_HIP(hipMemcpyAsync(out, dst, (size_t)B * c.proj_dim * 4, hipMemcpyDeviceToHost, s));
+  MRAG_HIP(hipStreamSynchronize(s));
+  return MRAG_OK;
+}
+
+int mrag_encoder_embed_tokens(mrag_encoder* e, const int32_t* ids, const int32_t* mask, int32_t batch, int32_t seq,
+                              float* out, int32_t normalize, int32_t ptr_kind, void* stream_arg) {
+  MRAG_REQUIRE(e != nullptr, "NULL encoder");
+  MRAG_REQUIRE(e->cfg.kind == MRAG_ENC_CLIP_TEXT || e->cfg.kind == MRAG_ENC_BERT, "not a text encoder");
+  MRAG_REQUIRE(batch >= 0 && seq >= 1, "bad shape batch=%d seq=%d", batch, seq);
+  MRAG_REQUIRE(seq <= e->cfg.max_positions && seq <= 256, "seq %d exceeds max positions (%d) or 256", seq,
+               e->cfg.max_positions);
+  MRAG_REQUIRE(ptr_kind == MRAG_PTR_HOST || ptr_kind == MRAG_PTR_DEVICE, "bad ptr_kind");
+  std::lock_guard<std::mutex> lk(e->mu);
+  mrag::DeviceGuard g(e->device);
+  if (int rc = check_ready(e)) return rc;
+  if (batch == 0) return MRAG_OK;
+  MRAG_REQUIRE(ids && out, "NULL ids/out");
+  hipStream_t s = stream_arg ? (hipStream_t)stream_arg : e->stream;
+  const auto& c = e->cfg;
+  const int B = batch, T = seq, D = c.hidden;
+  if (int rc = ensure_workspace(e, B, T)) return rc;
+  const int32_t* dids = ids;
+  const int32_t* dmask = mask;
+  if (ptr_kind == MRAG_PTR_HOST) {
+    if (int rc = buf_ensure(e->IDS, (size_t)B * T * 4)) return rc;
+    MRAG_HIP(hipMemcpyAsync(e->IDS.p, ids, (size_t)B * T * 4, hipMemcpyHostToDevice, s));
+    dids = (const int32_t*)e->IDS.p;
+    if (mask) {
+      if (int rc = buf_ensure(e->MASK, (size_t)B * T * 4)) return rc;
+      MRAG_HIP(hipMemcpyAsync(e->MASK.p, mask, (size_t)B * T * 4, hipMemcpyHostToDevice, s));
+      dmask = (const int32_t*)e->MASK.p;
+    }
+  }
+  float* X = (float*)e->X.p;
+  _Float16* H = (_Float16*)e->H16.p;
+  const int outD = c.kind == MRAG_ENC_BERT ? D : c.proj_dim;
+  float* dst = out;
+  if (ptr_kind == MRAG_PTR_HOST) {
+    if (int rc = buf_ensure(e->OUT, (size_t)B * outD * 4)) return rc;
+    dst = (float*)e->OUT.p;
+  }
+  if (c.kind == MRAG_ENC_CLIP_TEXT) {
+    if (int rc = launch_token_embed(dids, (const float*)e->tok.p, (const float*)e->pos.p, nullptr, X, B, T, D, c.vocab,
+                                    s))
+      return rc;
+    for (int i = 0; i < c.layers; ++i)
+      if (int rc = clip_layer(e, e->layers[i], B, T, dmask, 1, s)) return rc;
+    if (int rc = launch_eos_rows(dids, B, T, c.eos_token_id, (int*)e->ROWS.p, s)) return rc;
+    if (int rc = layernorm(X, (const int*)e->ROWS.p, nullptr, (_Float16*)e->POOL16.p, e->post_g, e->post_b, B, D,
+                           c.ln_eps, s))
+      return rc;
+    if (int rc = gemm(e->POOL16.p, e->proj_w.p, nullptr, dst, B, c.proj_dim, D, c.proj_dim, EPI_F32, s)) return rc;
+  } else {
+    if (int rc = launch_token_embed(dids, (const float*)e->tok.p, (const float*)e->pos.p, (const float*)e->type0.p, X,
+                                    B, T, D, c.vocab, s))
+      return rc;
+    if (int rc = layernorm(X, nullptr, X, H, e->emb_g, e->emb_b, B * T, D, c.ln_eps, s)) return rc;
+    for (int i = 0; i < c.layers; ++i)
+      if (int rc = bert_layer(e, e->layers[i], B, T, dmask, s)) return rc;
+    if (int rc = launch_mean_pool(X, dmask, dst, B, T, D, s)) return rc;
+  }
+  if (normalize)
+    if (int rc = mrag_l2norm_rows(dst, dst, B, outD, s)) return rc;
+  if (ptr_kind == MRAG_PTR_HOST) MRAG_HIP(hipMemcpyAsync(out, dst, (size_t)B * outD * 4, hipMemcpyDeviceToHost, s));
+  MRAG_HIP(hipStreamSynchronize(s));
+  return MRAG_OK;
+}
+
+int mrag_gemm_nt(const void* A, const void* W, const float* bias, void* C, int32_t M, int32_t N, int32_t K,
+                 int32_t epilogue, void* stream) {
+  MRAG_REQUIRE(A && W && C, "NULL pointer");
+  MRAG_REQUIRE(M >= 0 && N > 0 && K > 0, "bad shape");
+  return gemm(A, W, bias, C, M, N, K, N, epilogue, (hipStream_t)stream);
+}
+
+}  // extern "C"

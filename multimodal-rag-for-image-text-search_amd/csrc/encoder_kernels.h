@@ -1,0 +1,55 @@
+// encoder_kernels.h — argument blocks and launchers of the encoder kernels (K1..K5).
+#pragma once
+
+#include "common.h"
+
+namespace mrag_enc {
+
+enum Epilogue {
+  EPI_F16 = 0,             // C16 = acc + bias
+  EPI_F16_QUICK_GELU = 1,  // C16 = quick_gelu(acc + bias)       (CLIP MLP fc1)
+  EPI_F16_GELU_ERF = 2,    // C16 = gelu_erf(acc + bias)         (BERT intermediate)
+  EPI_F32_RESIDUAL = 3,    // C32 += acc + bias                  (out-proj / fc2 into the residual)
+  EPI_F32 = 4,             // C32 = acc + bias                   (patch embed, projections)
+};
+
+struct GemmArgs {
+  const _Float16* A;  // [M][lda]
+  const _Float16* W;  // [N][ldw]
+  const float* bias;  // [N] or null
+  void* C;            // [M][ldc] f16 or f32 per epilogue
+  int M, N, K, lda, ldw, ldc;
+};
+
+struct LayerNormArgs {
+  const float* x;      // [*][ldx]
+  const int* gather;   // optional: output row r reads input row gather[r]
+  float* y32;          // optional [rows][D]
+  _Float16* y16;       // optional [rows][D]
+  const float* gamma;
+  const float* beta;
+  int rows, D, ldx;
+  float eps;
+};
+
+struct AttentionArgs {
+  const _Float16* qkv;   // [B*L][3*H*dh]
+  _Float16* out;         // [B*L][H*dh]
+  const int32_t* mask;   // [B][L] key padding mask (1 = keep) or null
+  int B, L, H, causal;
+  float scale;
+};
+
+int launch_gemm(const GemmArgs& g, int epi, hipStream_t s);
+int launch_layernorm(const LayerNormArgs& a, hipStream_t s);
+int launch_attention(const AttentionArgs& a, int dh, hipStream_t s);
+int launch_vit_im2col(const uint8_t* img, _Float16* out, int B, int S, int P, hipStream_t s);
+int launch_vit_assemble(const float* patch, const float* cls, const float* pos, float* X, int B, int T, int D,
+                        hipStream_t s);
+int launch_token_embed(const int32_t* ids, const float* tok, const float* pos, const float* type0, float* X, int B,
+                       int T, int D, int vocab, hipStream_t s);
+int launch_eos_rows(const int32_t* ids, int B, int T, int eos_id, int* rows, hipStream_t s);
+int launch_cls_rows(int B, int T, int* rows, hipStream_t s);
+int launch_mean_pool(const float* X, const int32_t* mask, float* out, int B, int T, int D, hipStream_t s);
+
+}  // namespace mrag_enc

@@ -1,0 +1,430 @@
+// encoder_kernels.hip — K1..K5: the transformer building blocks of the three encoders
+// (CLIP ViT-B/32 image tower, CLIP text tower, MiniLM-L6 BERT), gfx950 only.
+//
+// Reference arithmetic (third-party, reached from app/ml/embeddings.py:62-105):
+//   transformers/models/clip/modeling_clip.py  CLIPVisionEmbeddings (:202-218), CLIPAttention
+//   (:280-335, scale head_dim^-0.5), CLIPMLP quick_gelu (:346-350), CLIPEncoderLayer pre-LN
+//   (:362-383), pooling (:561-580, :650-651), projections (:674-675, :750-751);
+//   transformers/models/bert/modeling_bert.py  embeddings + post-LN layers (:53-350).
+//
+// Layout: activations row-major [tokens][features]; the residual stream is f32, every GEMM
+// input is f16 (LayerNorm writes the f16 copy), weights are f16 [out][in] (torch Linear
+// layout, K contiguous for both GEMM operands), biases / LN params / embeddings f32.
+#include "common.h"
+#include "encoder_kernels.h"
+
+#define AS3 __attribute__((address_space(3)))
+
+namespace mrag_enc {
+
+__device__ __forceinline__ void glds_x4(const void* gsrc, uint32_t lds_addr) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(lds_addr)
+      : "memory");
+}
+
+// ---------------------------------------------------------------------------
+// K3: C[m][n] (+)= act(sum_k A[m][k] W[n][k] + bias[n])   (the "NT" GEMM of nn.Linear)
+// 128x128x64 block tile, 4 waves (2x2) of 64x64, MFMA 32x32x16 f16 -> f32.
+// Operands staged to LDS by LDS-DMA, 128-byte rows with chunk c stored at position
+// c ^ ((row >> 1) & 7) (source-address swizzle) so every ds_read_b128 fragment read is
+// bank-conflict free; 2 stages, one barrier per 64-deep k-step.
+constexpr int GM = 128, GN = 128, GK = 64;
+constexpr int GTHREADS = 256;
+constexpr int STAGE_BYTES = (GM + GN) * GK * 2;  // 32 KiB
+
+template <int EPI>
+__global__ __launch_bounds__(GTHREADS) void gemm_nt_kernel(GemmArgs g) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_BYTES];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = w >> 1, wc = w & 1;
+  const int h = lane >> 5, r32 = lane & 31;
+  const uint32_t lds_base = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)((AS3 char*)smem));
+
+  const int tiles_n = g.N / GN;
+  // consecutive blocks walk N for a fixed M panel (the A panel stays L2-resident)
+  const int tm = blockIdx.x / tiles_n, tn = blockIdx.x - (blockIdx.x / tiles_n) * tiles_n;
+  const int m0 = tm * GM, n0 = tn * GN;
+  const int ksteps = g.K / GK;
+
+  auto stage = [&](int buf, int k0) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int P = w * 8 + i;  // 1 KiB piece: 8 rows of 128 B
+      const int rr = lane >> 3, pos = lane & 7;
+      const int row = 8 * (P & 15) + rr;
+      const int c = pos ^ ((row >> 1) & 7);
+      const _Float16* src;
+      if (P < 16) {
+        const int m = min(m0 + row, g.M - 1);
+        src = g.A + (size_t)m * g.lda + k0 + c * 8;
+      } else {
+        src = g.W + (size_t)(n0 + row) * g.ldw + k0 + c * 8;
+      }
+      glds_x4(src, lds_base + buf * STAGE_BYTES + P * 1024);
+    }
+  };
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
+
+  const int sw = (r32 >> 1) & 7;
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int ks = 0; ks < ksteps; ++ks) {
+    const int cur = ks & 1;
+    if (ks + 1 < ksteps) stage(cur ^ 1, (ks + 1) * GK);
+    const char* At = (const char*)smem + cur * STAGE_BYTES;
+    const char* Bt = At + GM * GK * 2;
+#pragma unroll
+    for (int kk = 0; kk < GK / 16; ++kk) {
+      const int coff = (((2 * kk + h) ^ sw) * 16);
+      half8 a[2], b[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) a[i] = *(const half8*)(At + (wr * 64 + i * 32 + r32) * 128 + coff);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) b[j] = *(const half8*)(Bt + (wc * 64 + j * 32 + r32) * 128 + coff);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  // epilogue: lane owns column n of each 32x32 block and rows (reg&3)+8(reg>>2)+4h
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int n = n0 + wc * 64 + j * 32 + r32;
+    const float bn = g.bias ? g.bias[n] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) {
+        const int m = m0 + wr * 64 + i * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+        if (m >= g.M) continue;
+        float v = acc[i][j][reg] + bn;
+        const size_t o = (size_t)m * g.ldc + n;
+        if constexpr (EPI == EPI_F16) {
+          ((_Float16*)g.C)[o] = (_Float16)v;
+        } else if constexpr (EPI == EPI_F16_QUICK_GELU) {
+          v = v / (1.0f + __expf(-1.702f * v));
+          ((_Float16*)g.C)[o] = (_Float16)v;
+        } else if constexpr (EPI == EPI_F16_GELU_ERF) {
+          v = 0.5f * v * (1.0f + erff(v * 0.70710678118654752f));
+          ((_Float16*)g.C)[o] = (_Float16)v;
+        } else if constexpr (EPI == EPI_F32_RESIDUAL) {
+          ((float*)g.C)[o] += v;
+        } else {
+          ((float*)g.C)[o] = v;
+        }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// K2: LayerNorm over rows of D <= 1024 (one wave per row, two-pass mean/var in f32).
+// Optional row gather (pooling), f32 and/or f16 outputs (in-place f32 allowed).
+__global__ __launch_bounds__(256) void layernorm_kernel(LayerNormArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= a.rows) return;
+  const int src = a.gather ? a.gather[r] : r;
+  const float* x = a.x + (size_t)src * a.ldx;
+  float v[16];
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int d = lane + 64 * j;
+    v[j] = d < a.D ? x[d] : 0.f;
+    s += v[j];
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+  const float mean = s / (float)a.D;
+  float q = 0.f;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int d = lane + 64 * j;
+    const float t = d < a.D ? v[j] - mean : 0.f;
+    q += t * t;
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) q += __shfl_xor(q, off);
+  const float rstd = rsqrtf(q / (float)a.D + a.eps);
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int d = lane + 64 * j;
+    if (d < a.D) {
+      const float y = (v[j] - mean) * rstd * a.gamma[d] + a.beta[d];
+      if (a.y32) a.y32[(size_t)r * a.D + d] = y;
+      if (a.y16) a.y16[(size_t)r * a.D + d] = (_Float16)y;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// K4: multi-head attention for short sequences (L <= 256): one workgroup per
+// (sequence, head), K and V of the head in LDS (f32), one thread per query row with
+// an online softmax over the keys (key padding mask, optional causal mask).
+// qkv: [B*L][3*D] f16 (q | k | v, head h at columns h*DH), out: [B*L][D] f16.
+template <int DH>
+__global__ __launch_bounds__(256) void attention_kernel(AttentionArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sh[];
+  float* Ks = sh;                       // [L][DH]
+  float* Vs = sh + a.L * DH;            // [L][DH]
+  int* valid = (int*)(sh + 2 * a.L * DH);  // [L]
+  const int b = blockIdx.x / a.H, hd = blockIdx.x - (blockIdx.x / a.H) * a.H;
+  const int D = a.H * DH;
+  const size_t rs = (size_t)3 * D;
+  const _Float16* base = a.qkv + (size_t)b * a.L * rs;
+  for (int idx = threadIdx.x; idx < a.L * DH; idx += blockDim.x) {
+    const int t = idx / DH, d = idx - (idx / DH) * DH;
+    Ks[idx] = (float)base[t * rs + D + hd * DH + d];
+    Vs[idx] = (float)base[t * rs + 2 * D + hd * DH + d];
+  }
+  for (int t = threadIdx.x; t < a.L; t += blockDim.x) valid[t] = a.mask ? (a.mask[b * a.L + t] != 0) : 1;
+  __syncthreads();
+  const int i = threadIdx.x;
+  if (i >= a.L) return;
+  float q[DH], o[DH];
+  const _Float16* qr = base + i * rs + hd * DH;
+#pragma unroll
+  for (int d = 0; d < DH; ++d) {
+    q[d] = (float)qr[d] * a.scale;
+    o[d] = 0.f;
+  }
+  float m = -INFINITY, l = 0.f;
+  const int jend = a.causal ? i + 1 : a.L;
+  for (int j = 0; j < jend; ++j) {
+    if (!valid[j]) continue;
+    const float* kr = Ks + j * DH;
+    float s = 0.f;
+#pragma unroll
+    for (int d = 0; d < DH; ++d) s = fmaf(q[d], kr[d], s);
+    const float mn = fmaxf(m, s);
+    const float alpha = __expf(m - mn);
+    const float p = __expf(s - mn);
+    l = l * alpha + p;
+    const float* vr = Vs + j * DH;
+#pragma unroll
+    for (int d = 0; d < DH; ++d) o[d] = fmaf(p, vr[d], o[d] * alpha);
+    m = mn;
+  }
+  const float inv = l > 0.f ? 1.f / l : 0.f;
+  _Float16* orow = a.out + ((size_t)b * a.L + i) * D + hd * DH;
+#pragma unroll
+  for (int d = 0; d < DH; ++d) orow[d] = (_Float16)(o[d] * inv);
+}
+
+// ---------------------------------------------------------------------------
+// K1 (prologue): CLIP pixel normalisation fused into the patch im2col.
+// Reference: CLIPImageProcessor rescale (u8 -> f64 * 1/255 -> f32) then (x - mean) / std
+// in f32 (app/ml/embeddings.py:85; bit-exact formula verified in SURVEY.md §8a a2), then the
+// Conv2d(3, 768, k=32, s=32) as a GEMM with K ordered (c, kh, kw) like the torch weight.
+// img: [B][S][S][3] u8 (HWC, the decoded RGB image), out: [B*G*G][3*P*P] f16.
+__global__ void vit_im2col_kernel(const uint8_t* __restrict__ img, _Float16* __restrict__ out, int B, int S,
+                                  int P) {
+  const int G = S / P;
+  const int K = 3 * P * P;
+  const int64_t total8 = (int64_t)B * G * G * (K / 8);
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= total8) return;
+  const int64_t row = idx / (K / 8);
+  const int k8 = (int)(idx - row * (K / 8)) * 8;
+  const int c = k8 / (P * P), kh = (k8 / P) % P, kw0 = k8 % P;
+  const int b = (int)(row / (G * G)), pidx = (int)(row % (G * G));
+  const int py = pidx / G, px = pidx % G;
+  const float mean = c == 0 ? 0.48145466f : (c == 1 ? 0.4578275f : 0.40821073f);
+  const float stdv = c == 0 ? 0.26862954f : (c == 1 ? 0.26130258f : 0.27577711f);
+  const uint8_t* src = img + (((size_t)b * S + (size_t)py * P + kh) * S + (size_t)px * P + kw0) * 3 + c;
+  _Float16 v8[8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    const float x = (float)((double)src[t * 3] * (1.0 / 255.0));
+    v8[t] = (_Float16)((x - mean) / stdv);
+  }
+  *(half8*)(out + row * K + k8) = *(half8*)v8;
+}
+
+// X[b*T + t] = (t == 0 ? cls : patch[b*(T-1) + t-1]) + pos[t]   (f32)
+__global__ void vit_assemble_kernel(const float* __restrict__ patch, const float* __restrict__ cls,
+                                    const float* __restrict__ pos, float* __restrict__ X, int B, int T, int D) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (int64_t)B * T * D) return;
+  const int d = (int)(idx % D);
+  const int64_t bt = idx / D;
+  const int t = (int)(bt % T);
+  const int64_t b = bt / T;
+  const float e = t == 0 ? cls[d] : patch[(b * (T - 1) + t - 1) * D + d];
+  X[idx] = e + pos[(size_t)t * D + d];
+}
+
+// Token embeddings: X[b*T+t] = tok[ids] + pos[t] (+ type0 for BERT)   (f32)
+__global__ void token_embed_kernel(const int32_t* __restrict__ ids, const float* __restrict__ tok,
+                                   const float* __restrict__ pos, const float* __restrict__ type0,
+                                   float* __restrict__ X, int B, int T, int D, int vocab) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (int64_t)B * T * D) return;
+  const int d = (int)(idx % D);
+  const int64_t bt = idx / D;
+  const int t = (int)(bt % T);
+  int id = ids[bt];
+  id = id < 0 ? 0 : (id >= vocab ? vocab - 1 : id);
+  float e = tok[(size_t)id * D + d] + pos[(size_t)t * D + d];
+  if (type0) e += type0[d];
+  X[idx] = e;
+}
+
+// CLIP text pooling row per sequence: first index of eos_id (eos_id >= 0) or argmax of
+// the ids (legacy configs with eos_token_id == 2), modeling_clip.py:561-580.
+__global__ void eos_rows_kernel(const int32_t* __restrict__ ids, int B, int T, int eos_id, int* __restrict__ rows) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const int32_t* r = ids + (size_t)b * T;
+  int best = 0;
+  if (eos_id >= 0) {
+    for (int t = 0; t < T; ++t)
+      if (r[t] == eos_id) {
+        best = t;
+        break;
+      }
+  } else {
+    int bv = r[0];
+    for (int t = 1; t < T; ++t)
+      if (r[t] > bv) {
+        bv = r[t];
+        best = t;
+      }
+  }
+  rows[b] = b * T + best;
+}
+
+// Rows b*T (the CLS token of each image).
+__global__ void cls_rows_kernel(int B, int T, int* __restrict__ rows) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b < B) rows[b] = b * T;
+}
+
+// sentence-transformers mean pooling: sum_t(h*m) / clamp(sum_t m, 1e-9)
+__global__ void mean_pool_kernel(const float* __restrict__ X, const int32_t* __restrict__ mask,
+                                 float* __restrict__ out, int B, int T, int D) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (int64_t)B * D) return;
+  const int b = (int)(idx / D), d = (int)(idx % D);
+  float s = 0.f, c = 0.f;
+  for (int t = 0; t < T; ++t) {
+    const float mm = mask ? (float)(mask[(size_t)b * T + t] != 0) : 1.f;
+    s += X[((size_t)b * T + t) * D + d] * mm;
+    c += mm;
+  }
+  out[idx] = s / fmaxf(c, 1e-9f);
+}
+
+// ---------------------------------------------------------------------------
+// launchers
+int launch_gemm(const GemmArgs& g, int epi, hipStream_t s) {
+  if (g.M <= 0) return MRAG_OK;
+  MRAG_REQUIRE(g.N % GN == 0 && g.K % GK == 0, "gemm: N=%d must be a multiple of %d and K=%d of %d", g.N, GN, g.K,
+               GK);
+  MRAG_REQUIRE(g.lda % 8 == 0 && g.ldw % 8 == 0, "gemm: lda/ldw must be multiples of 8");
+  const dim3 grid((unsigned)(((g.M + GM - 1) / GM) * (g.N / GN)));
+  switch (epi) {
+    case EPI_F16: hipLaunchKernelGGL(gemm_nt_kernel<EPI_F16>, grid, dim3(GTHREADS), 0, s, g); break;
+    case EPI_F16_QUICK_GELU: hipLaunchKernelGGL(gemm_nt_kernel<EPI_F16_QUICK_GELU>, grid, dim3(GTHREADS), 0, s, g); break;
+    case EPI_F16_GELU_ERF: hipLaunchKernelGGL(gemm_nt_kernel<EPI_F16_GELU_ERF>, grid, dim3(GTHREADS), 0, s, g); break;
+    case EPI_F32_RESIDUAL: hipLaunchKernelGGL(gemm_nt_kernel<EPI_F32_RESIDUAL>, grid, dim3(GTHREADS), 0, s, g); break;
+    case EPI_F32: hipLaunchKernelGGL(gemm_nt_kernel<EPI_F32>, grid, dim3(GTHREADS), 0, s, g); break;
+    default: return mrag::fail(MRAG_ERR_ARG, "gemm: bad epilogue %d", epi);
+  }
+  MRAG_CHECK_LAUNCH();
+  return MRAG_OK;
+}
+
+int launch_layernorm(const LayerNormArgs& a, hipStream_t s) {
+  if (a.rows <= 0) return MRAG_OK;
+  MRAG_REQUIRE(a.D > 0 && a.D <= 1024, "layernorm: D=%d unsupported", a.D);
+  hipLaunchKernelGGL(layernorm_kernel, dim3((unsigned)((a.rows + 3) / 4)), dim3(256), 0, s, a);
+  MRAG_CHECK_LAUNCH();
+  return MRAG_OK;
+}
+
+int launch_attention(const AttentionArgs& a, int dh, hipStream_t s) {
+  if (a.B <= 0) return MRAG_OK;
+  MRAG_REQUIRE(a.L >= 1 && a.L <= 256, "attention: L=%d unsupported (1..256)", a.L);
+  const size_t shm = (size_t)2 * a.L * dh * 4 + (size_t)a.L * 4;
+  MRAG_REQUIRE(shm <= 65536, "attention: L*dh too large for LDS");
+  const int threads = (a.L + 63) / 64 * 64;
+  const dim3 grid((unsigned)(a.B * a.H));
+  if (dh == 64) {
+    hipLaunchKernelGGL(attention_kernel<64>, grid, dim3(threads), shm, s, a);
+  } else if (dh == 32) {
+    hipLaunchKernelGGL(attention_kernel<32>, grid, dim3(threads), shm, s, a);
+  } else {
+    return mrag::fail(MRAG_ERR_UNSUPPORTED, "attention: head_dim %d unsupported (32, 64)", dh);
+  }
+  MRAG_CHECK_LAUNCH();
+  return MRAG_OK;
+}
+
+int launch_vit_im2col(const uint8_t* img, _Float16* out, int B, int S, int P, hipStream_t s) {
+  const int64_t total8 = (int64_t)B * (S / P) * (S / P) * (3 * P * P / 8);
+  if (total8 == 0) return MRAG_OK;
+  hipLaunchKernelGGL(vit_im2col_kernel, dim3((unsigned)((total8 + 255) / 256)), dim3(256), 0, s, img, out, B, S, P);
+  MRAG_CHECK_LAUNCH();
+  return MRAG_OK;
+}
+
+int launch_vit_assemble(const float* patch, const float* cls, const float* pos, float* X, int B, int T, int D,
+                        hipStream_t s) {
+  const int64_t n = (int64_t)B * T * D;
+  if (n == 0) return MRAG_OK;
+  hipLaunchKernelGGL(vit_assemble_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, patch, cls, pos, X, B,
+                     T, D);
+  MRAG_CHECK_LAUNCH();
+  return MRAG_OK;
+}
+
+int launch_token_embed(const int32_t* ids, const float* tok, const float* pos, const float* type0, float* X, int B,
+                       int T, int D, int vocab, hipStream_t s) {
+  const int64_t n = (int64_t)B * T * D;
+  if (n == 0) return MRAG_OK;
+  hipLaunchKernelGGL(token_embed_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, ids, tok, pos, type0, X,
+                     B, T, D, vocab);
+  MRAG_CHECK_LAUNCH();
+  return MRAG_OK;
+}
+
+int launch_eos_rows(const int32_t* ids, int B, int T, int eos_id, int* rows, hipStream_t s) {
+  if (B == 0) return MRAG_OK;
+  hipLaunchKernelGGL(eos_rows_kernel, dim3((unsigned)((B + 63) / 64)), dim3(64), 0, s, ids, B, T, eos_id, rows);
+  MRAG_CHECK_LAUNCH();
+  return MRAG_OK;
+}
+
+int launch_cls_rows(int B, int T, int* rows, hipStream_t s) {
+  if (B == 0) return MRAG_OK;
+  hipLaunchKernelGGL(cls_rows_kernel, dim3((unsigned)((B + 63) / 64)), dim3(64), 0, s, B, T, rows);
+  MRAG_CHECK_LAUNCH();
+  return MRAG_OK;
+}
+
+int launch_mean_pool(const float* X, const int32_t* mask, float* out, int B, int T, int D, hipStream_t s) {
+  const int64_t n = (int64_t)B * D;
+  if (n == 0) return MRAG_OK;
+  hipLaunchKernelGGL(mean_pool_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, X, mask, out, B, T, D);
+  MRAG_CHECK_LAUNCH();
+  return MRAG_OK;
+}
+
+}  // namespace mrag_enc

@@ -1,0 +1,126 @@
+"""Torch-CPU fp32 restatement of the three encoder forwards (test oracle only).
+
+The reference's numerics live in transformers / sentence-transformers
+(app/ml/embeddings.py:26-43, 62-105). Here the same architectures are instantiated
+from the installed transformers (5.15.0; the reference pins none) with the
+deterministic synthetic weights of ``app/encoders/weights.py`` loaded by state-dict
+name, and the pieces sentence-transformers would add (not installed) are restated:
+
+* CLIP image: pixel normalisation ``((f32)(u8 * (1/255 as f64)) - mean) / std``
+  (CLIPImageProcessor) -> ``get_image_features(...).pooler_output``
+  (transformers 5.x returns BaseModelOutputWithPooling; the reference's ``.detach()``
+  at app/ml/embeddings.py:89 predates that) -> reference ``_normalize``.
+* CLIP text: ``get_text_features(ids, mask).pooler_output`` -> ``_normalize``.
+* MiniLM: ``BertModel`` last hidden state -> mean pooling ``sum(h*m)/clamp(sum m, 1e-9)``
+  -> ``F.normalize(p=2, eps=1e-12)`` (sentence-transformers Pooling + Normalize) ->
+  ``_normalize`` (app/ml/embeddings.py:69-70).
+"""
+from __future__ import annotations
+
+import importlib.util
+import math
+import os
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+_WEIGHTS = os.path.join(ROOT, "multimodal-rag-for-image-text-search_amd", "app", "encoders", "weights.py")
+
+CLIP_MEAN = np.array([0.48145466, 0.4578275, 0.40821073], dtype=np.float32)
+CLIP_STD = np.array([0.26862954, 0.26130258, 0.27577711], dtype=np.float32)
+
+
+def weights_module():
+    """The product's weight generator, loaded by path (no `app` package import, so this
+    also works in a process where the reference's own `app` package is imported)."""
+    import sys
+
+    if "mrag_weights" in sys.modules:
+        return sys.modules["mrag_weights"]
+    spec = importlib.util.spec_from_file_location("mrag_weights", _WEIGHTS)
+    mod = importlib.util.module_from_spec(spec)
+    sys.modules["mrag_weights"] = mod  # dataclasses need the module registered
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def normalize_rows(x: np.ndarray) -> np.ndarray:
+    """app/ml/embeddings.py:46-49 `_normalize`, restated."""
+    norms = np.linalg.norm(x, axis=1, keepdims=True)
+    norms[norms == 0] = 1.0
+    return x / norms
+
+
+def pixel_values(images_u8: np.ndarray) -> np.ndarray:
+    """u8 [B,H,W,3] -> f32 NCHW, CLIPImageProcessor rescale+normalise order."""
+    x = (images_u8.astype(np.float64) * (1.0 / 255.0)).astype(np.float32)
+    x = (x - CLIP_MEAN) / CLIP_STD
+    return np.ascontiguousarray(x.transpose(0, 3, 1, 2))
+
+
+def clip_model(seed: int = 0):
+    import torch
+    from transformers import CLIPConfig, CLIPModel
+
+    w = weights_module()
+    model = CLIPModel(CLIPConfig()).eval()
+    sd = {}
+    for cfg in (w.CLIP_VISION_B32, w.CLIP_TEXT_B32):
+        for name, arr in w.synth_state_dict(cfg, seed):
+            sd[name] = torch.from_numpy(arr)
+    sd["logit_scale"] = torch.tensor(math.log(1 / 0.07))
+    missing, unexpected = model.load_state_dict(sd, strict=False)
+    assert not unexpected, unexpected
+    assert all("position_ids" in m for m in missing), missing
+    return model
+
+
+def bert_model(seed: int = 0):
+    import torch
+    from transformers import BertConfig, BertModel
+
+    w = weights_module()
+    c = w.MINILM_L6
+    cfg = BertConfig(vocab_size=c.vocab, hidden_size=c.hidden, num_hidden_layers=c.layers,
+                     num_attention_heads=c.heads, intermediate_size=c.intermediate,
+                     max_position_embeddings=c.max_positions, hidden_act="gelu", layer_norm_eps=c.ln_eps)
+    model = BertModel(cfg, add_pooling_layer=False).eval()
+    sd = {n: torch.from_numpy(a) for n, a in w.synth_state_dict(c, seed)}
+    missing, unexpected = model.load_state_dict(sd, strict=False)
+    assert not unexpected, unexpected
+    assert all("position_ids" in m or "token_type_ids" in m for m in missing), missing
+    return model
+
+
+def clip_image_embeds(model, images_u8: np.ndarray, normalize: bool = True) -> np.ndarray:
+    import torch
+
+    with torch.no_grad():
+        out = model.get_image_features(pixel_values=torch.from_numpy(pixel_values(images_u8))).pooler_output
+    arr = out.float().numpy()
+    return normalize_rows(arr) if normalize else arr
+
+
+def clip_text_embeds(model, ids: np.ndarray, mask: np.ndarray, normalize: bool = True) -> np.ndarray:
+    import torch
+
+    with torch.no_grad():
+        out = model.get_text_features(input_ids=torch.from_numpy(ids.astype(np.int64)),
+                                      attention_mask=torch.from_numpy(mask.astype(np.int64))).pooler_output
+    arr = out.float().numpy()
+    return normalize_rows(arr) if normalize else arr
+
+
+def minilm_embeds(model, ids: np.ndarray, mask: np.ndarray, normalize: bool = True) -> np.ndarray:
+    import torch
+    import torch.nn.functional as F
+
+    with torch.no_grad():
+        h = model(input_ids=torch.from_numpy(ids.astype(np.int64)),
+                  attention_mask=torch.from_numpy(mask.astype(np.int64))).last_hidden_state
+        m = torch.from_numpy(mask.astype(np.float32)).unsqueeze(-1)
+        pooled = (h * m).sum(1) / torch.clamp(m.sum(1), min=1e-9)
+        if not normalize:
+            return pooled.numpy()
+        pooled = F.normalize(pooled, p=2, dim=1, eps=1e-12)
+    return normalize_rows(pooled.numpy())
