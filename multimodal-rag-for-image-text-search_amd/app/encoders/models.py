@@ -1,0 +1,143 @@
+"""Model objects with the call signatures the reference's embedding helpers use, so the
+module-global seams of ``app/ml/embeddings.py`` (``_TEXT_MODEL``, ``_CLIP_MODEL``,
+``_CLIP_PROCESSOR``) keep working — the tests monkeypatch them with dummies exactly
+as the reference's tests do (tests/test_embeddings.py:14-57).
+
+* ``MiniLMSentenceModel.encode(...)``  ~ SentenceTransformer.encode (all-MiniLM-L6-v2:
+  WordPiece -> BERT -> mean pooling -> Normalize), on the GPU encoder.
+* ``ClipModel.get_image_features / get_text_features``  ~ CLIPModel's, returning the
+  projected features as a CUDA tensor.
+* ``ClipProcessor(images=... | text=...)``  ~ CLIPProcessor: host decode/resize/crop to
+  u8 224x224 (normalisation is fused on the GPU) and CLIP tokenisation.
+"""
+from __future__ import annotations
+
+import json
+import os
+from typing import Optional, Sequence
+
+import numpy as np
+
+from app.encoders import CLIP_TEXT_B32, CLIP_VISION_B32, MINILM_L6, load_encoder
+from app.encoders.preprocess import load_batch
+from app.encoders.tokenize import ClipTokenizer, WordPieceTokenizer
+
+
+def _device_index() -> int:
+    return int(os.environ.get("MRAG_DEVICE", "0"))
+
+
+def _local_dir(name: Optional[str]) -> Optional[str]:
+    return name if name and os.path.isdir(name) else None
+
+
+class BatchInputs(dict):
+    """dict with ``.to(device)`` and attribute access (BatchFeature stand-in)."""
+
+    def to(self, device):
+        return self
+
+    def __getattr__(self, k):
+        try:
+            return self[k]
+        except KeyError as e:
+            raise AttributeError(k) from e
+
+
+class MiniLMSentenceModel:
+    def __init__(self, name: Optional[str] = None, device: Optional[int] = None):
+        d = _local_dir(name)
+        self.device = _device_index() if device is None else device
+        self.enc = load_encoder(MINILM_L6, d, device=self.device)
+        self.tokenizer = WordPieceTokenizer(d, max_len=256)
+
+    def to(self, device):
+        return self
+
+    def encode(self, sentences: Sequence[str], batch_size: int = 32, convert_to_tensor: bool = False,
+               device=None, show_progress_bar=None, **kw):
+        import torch
+
+        sentences = list(sentences)
+        out = torch.empty((len(sentences), MINILM_L6.hidden), dtype=torch.float32, device=f"cuda:{self.device}")
+        if not sentences:
+            return out if convert_to_tensor else out.cpu().numpy()
+        # length-sorted batches like sentence-transformers; rows are independent, so the
+        # GPU batch is sized for throughput (>= the caller's batch_size)
+        order = np.argsort([-len(s) for s in sentences], kind="stable")
+        gb = max(int(batch_size), 256)
+        for s0 in range(0, len(order), gb):
+            idx = order[s0:s0 + gb]
+            ids, mask = self.tokenizer([sentences[i] for i in idx])
+            emb = self.enc.embed_tokens(torch.from_numpy(ids).to(out.device), torch.from_numpy(mask).to(out.device),
+                                        normalize=True)
+            out[torch.from_numpy(idx).to(out.device)] = emb
+        return out if convert_to_tensor else out.cpu().numpy()
+
+
+class ClipModel:
+    def __init__(self, name: Optional[str] = None, device: Optional[int] = None):
+        self.dir = _local_dir(name)
+        self.device = _device_index() if device is None else device
+        self._vision = None
+        self._text = None
+
+    def to(self, device):
+        return self
+
+    def _text_cfg(self):
+        cfg = CLIP_TEXT_B32
+        if self.dir and os.path.exists(os.path.join(self.dir, "config.json")):
+            tc = json.load(open(os.path.join(self.dir, "config.json"))).get("text_config", {})
+            eos = tc.get("eos_token_id", cfg.eos_token_id)
+            from dataclasses import replace
+
+            cfg = replace(cfg, eos_token_id=-1 if eos == 2 else int(eos))  # legacy configs pool at argmax(ids)
+        return cfg
+
+    @property
+    def vision(self):
+        if self._vision is None:
+            self._vision = load_encoder(CLIP_VISION_B32, self.dir, device=self.device)
+        return self._vision
+
+    @property
+    def text(self):
+        if self._text is None:
+            self._text = load_encoder(self._text_cfg(), self.dir, device=self.device)
+        return self._text
+
+    def get_image_features(self, images_u8=None, pixel_values=None, **kw):
+        import torch
+
+        if images_u8 is None:
+            raise TypeError("the GPU image tower takes u8 224x224 images (images_u8=), as produced by ClipProcessor")
+        x = images_u8 if isinstance(images_u8, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(images_u8))
+        return self.vision.embed_images(x.to(f"cuda:{self.device}"), normalize=False)
+
+    def get_text_features(self, input_ids=None, attention_mask=None, **kw):
+        import torch
+
+        ids = input_ids if isinstance(input_ids, torch.Tensor) else torch.from_numpy(np.asarray(input_ids))
+        dev = f"cuda:{self.device}"
+        m = None
+        if attention_mask is not None:
+            m = attention_mask if isinstance(attention_mask, torch.Tensor) else torch.from_numpy(np.asarray(attention_mask))
+            m = m.to(dev)
+        return self.text.embed_tokens(ids.to(dev), m, normalize=False)
+
+
+class ClipProcessor:
+    def __init__(self, name: Optional[str] = None):
+        self.tokenizer = ClipTokenizer(_local_dir(name))
+
+    def to(self, device):
+        return self
+
+    def __call__(self, *, images=None, text=None, return_tensors="pt", padding=None, **kw):
+        if images is not None:
+            return BatchInputs(images_u8=load_batch(list(images)))
+        if text is not None:
+            ids, mask = self.tokenizer(list(text))
+            return BatchInputs(input_ids=ids, attention_mask=mask)
+        raise ValueError("ClipProcessor needs images= or text=")

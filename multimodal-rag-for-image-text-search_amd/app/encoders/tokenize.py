@@ -1,0 +1,105 @@
+"""Host tokenisation for the text towers.
+
+The reference tokenises inside sentence-transformers (WordPiece, max_seq_length 256)
+and CLIPProcessor (BPE, padding=True, no truncation: >77 tokens raises), both loaded by
+hub name — unavailable offline. Two sources, in order:
+
+1. a local model directory (MODEL_TEXT / MODEL_CLIP) with ``vocab.txt`` (WordPiece)
+   or ``vocab.json`` + ``merges.txt`` (CLIP BPE): the real tokenisers (``tokenizers``
+   / transformers, installed);
+2. otherwise a deterministic hashing tokeniser with the same special tokens, lengths
+   and padding conventions (BERT-style basic pre-tokenisation; ids hashed into the
+   vocabulary). Embeddings then differ from the pretrained model's — only weights
+   loaded from a checkpoint make them meaningful — but shapes, masks, truncation and
+   throughput are those of the reference. Parity tests feed token ids directly.
+"""
+from __future__ import annotations
+
+import os
+import re
+import unicodedata
+import zlib
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+
+_PUNCT = re.compile(r"\w+|[^\w\s]", re.UNICODE)
+
+
+def _basic_tokens(text: str, lower: bool = True) -> List[str]:
+    t = unicodedata.normalize("NFC", text)
+    if lower:
+        t = t.lower()
+    return _PUNCT.findall(t)
+
+
+def _hash_id(tok: str, lo: int, hi: int) -> int:
+    return lo + zlib.crc32(tok.encode("utf-8")) % (hi - lo)
+
+
+class WordPieceTokenizer:
+    """MiniLM tokeniser: [CLS] ... [SEP], truncation to max_len (ST: 256)."""
+
+    CLS, SEP, PAD = 101, 102, 0
+
+    def __init__(self, model_dir: Optional[str] = None, max_len: int = 256, vocab: int = 30522):
+        self.max_len = max_len
+        self.vocab = vocab
+        self._tok = None
+        if model_dir and os.path.exists(os.path.join(model_dir, "vocab.txt")):
+            from tokenizers import BertWordPieceTokenizer
+
+            self._tok = BertWordPieceTokenizer(os.path.join(model_dir, "vocab.txt"), lowercase=True)
+
+    def encode_one(self, text: str) -> List[int]:
+        if self._tok is not None:
+            ids = self._tok.encode(text).ids  # includes [CLS]/[SEP]
+            if len(ids) > self.max_len:
+                ids = ids[: self.max_len - 1] + [self.SEP]
+            return ids
+        body = [_hash_id(t, 1000, self.vocab) for t in _basic_tokens(text)]
+        return [self.CLS] + body[: self.max_len - 2] + [self.SEP]
+
+    def __call__(self, texts: Sequence[str]) -> Tuple[np.ndarray, np.ndarray]:
+        seqs = [self.encode_one(t) for t in texts]
+        T = max(len(s) for s in seqs)
+        ids = np.full((len(seqs), T), self.PAD, dtype=np.int32)
+        mask = np.zeros((len(seqs), T), dtype=np.int32)
+        for i, s in enumerate(seqs):
+            ids[i, : len(s)] = s
+            mask[i, : len(s)] = 1
+        return ids, mask
+
+
+class ClipTokenizer:
+    """CLIP BPE: <|startoftext|> ... <|endoftext|>, padding=True (pad = EOS id), no
+    truncation; sequences longer than 77 raise like the reference's model call."""
+
+    BOS, EOS = 49406, 49407
+
+    def __init__(self, model_dir: Optional[str] = None, max_len: int = 77, vocab: int = 49408):
+        self.max_len = max_len
+        self.vocab = vocab
+        self._tok = None
+        if model_dir and os.path.exists(os.path.join(model_dir, "vocab.json")) and \
+                os.path.exists(os.path.join(model_dir, "merges.txt")):
+            from transformers import CLIPTokenizer
+
+            self._tok = CLIPTokenizer(os.path.join(model_dir, "vocab.json"), os.path.join(model_dir, "merges.txt"))
+
+    def encode_one(self, text: str) -> List[int]:
+        if self._tok is not None:
+            return list(self._tok(text)["input_ids"])
+        return [self.BOS] + [_hash_id(t, 256, self.BOS) for t in _basic_tokens(text)] + [self.EOS]
+
+    def __call__(self, texts: Sequence[str]) -> Tuple[np.ndarray, np.ndarray]:
+        seqs = [self.encode_one(t) for t in texts]
+        T = max(len(s) for s in seqs)
+        if T > self.max_len:
+            raise ValueError(f"Sequence length {T} exceeds the CLIP text maximum of {self.max_len} positions")
+        ids = np.full((len(seqs), T), self.EOS, dtype=np.int32)
+        mask = np.zeros((len(seqs), T), dtype=np.int32)
+        for i, s in enumerate(seqs):
+            ids[i, : len(s)] = s
+            mask[i, : len(s)] = 1
+        return ids, mask

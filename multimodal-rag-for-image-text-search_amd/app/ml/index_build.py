@@ -1,0 +1,114 @@
+"""Drop-in for the reference's ``app/ml/index_build.py``.
+
+``index_text_nodes`` (:46-103): documents -> sentence-split nodes -> metadata-prefixed
+texts -> ``embed_text_batch`` -> ``VectorRow``s -> ``upsert_text_vectors`` -> version
+bump. ``index_image_nodes`` (:106-155): drop nodes whose file is missing ->
+``embed_images_batch`` -> ``upsert_image_vectors`` -> version bump.
+``get_index_version`` keys the retrieval cache. Module globals ``_LANCEDB_STORE``,
+``_VERSION_FILE``, ``embed_text_batch``, ``embed_images_batch`` are looked up at call
+time, so tests can monkeypatch them as the reference's tests do. The version file is
+written atomically under a process lock (the reference's read-modify-write races).
+"""
+from __future__ import annotations
+
+import json
+import os
+import threading
+from pathlib import Path
+from typing import Dict, List, Sequence
+
+from app.ml.embeddings import embed_images_batch, embed_query_for_images, embed_text_batch
+from app.ml.splitter import Document, SentenceSplitter
+from app.settings import settings
+from app.storage.lancedb_store import LanceDBStore, VectorRow
+
+_SPLITTER = SentenceSplitter(chunk_size=512, chunk_overlap=64)
+_LANCEDB_STORE = LanceDBStore(settings.paths.lancedb_dir)
+_VERSION_FILE = Path(settings.paths.lancedb_dir) / "index_versions.json"
+_VERSION_LOCK = threading.Lock()
+
+
+def _load_versions() -> Dict[str, int]:
+    if not _VERSION_FILE.exists():
+        return {}
+    try:
+        return json.loads(_VERSION_FILE.read_text())
+    except Exception:
+        return {}
+
+
+def _save_versions(versions: Dict[str, int]) -> None:
+    _VERSION_FILE.parent.mkdir(parents=True, exist_ok=True)
+    tmp = _VERSION_FILE.with_suffix(".tmp")
+    tmp.write_text(json.dumps(versions))
+    os.replace(tmp, _VERSION_FILE)
+
+
+def _bump_version(user_id: str) -> int:
+    with _VERSION_LOCK:
+        versions = _load_versions()
+        versions[user_id] = versions.get(user_id, 0) + 1
+        _save_versions(versions)
+        return versions[user_id]
+
+
+def get_index_version(user_id: str) -> int:
+    return _load_versions().get(user_id, 0)
+
+
+def index_text_nodes(user_id: str, nodes: Sequence[Dict[str, object]]) -> List[Dict[str, object]]:
+    """Chunk and index text nodes ({id, text, metadata})."""
+    documents: List[Document] = []
+    for node in nodes:
+        text = str(node.get("text") or "").strip()
+        if not text:
+            continue
+        documents.append(Document(text=text, metadata=dict(node.get("metadata", {})), doc_id=str(node.get("id"))))
+    if not documents:
+        return []
+    parsed_nodes = _SPLITTER.get_nodes_from_documents(documents)
+    texts = [n.get_content(metadata_mode="all") for n in parsed_nodes]
+    if not texts:
+        return []
+    embeddings = embed_text_batch(texts)
+    rows: List[VectorRow] = []
+    stored: List[Dict[str, object]] = []
+    for parsed, embedding in zip(parsed_nodes, embeddings):
+        meta = dict(parsed.metadata)
+        meta.update({"doc_id": parsed.ref_doc_id or parsed.node_id, "user_id": user_id, "modality": "text",
+                     "source": meta.get("source")})
+        rows.append(VectorRow(chunk_id=parsed.node_id, user_id=user_id, document_id=meta["doc_id"], modality="text",
+                              embedding=embedding.tolist(), meta=meta))
+        stored.append({"chunk_id": parsed.node_id, "metadata": meta, "text": parsed.get_content(metadata_mode="none")})
+    if rows:
+        _LANCEDB_STORE.upsert_text_vectors(rows)
+        _bump_version(user_id)
+    return stored
+
+
+def index_image_nodes(user_id: str, nodes: Sequence[Dict[str, object]]) -> List[Dict[str, object]]:
+    """Index image nodes ({id, metadata{file_path, ...}}) with CLIP embeddings."""
+    paths: List[Path] = []
+    rows: List[VectorRow] = []
+    for node in nodes:
+        metadata = dict(node.get("metadata", {}))
+        file_path = Path(str(metadata.get("file_path", "")))
+        if not file_path.exists():
+            continue
+        chunk_id = str(node.get("id"))
+        metadata.update({"doc_id": metadata.get("doc_id", chunk_id), "user_id": user_id, "modality": "image",
+                         "source": metadata.get("source")})
+        paths.append(file_path)
+        rows.append(VectorRow(chunk_id=chunk_id, user_id=user_id, document_id=metadata["doc_id"], modality="image",
+                              embedding=[], meta=metadata))
+    if not rows:
+        return []
+    embeddings = embed_images_batch(paths)
+    for row, embedding in zip(rows, embeddings):
+        row.embedding = embedding.tolist()
+    _LANCEDB_STORE.upsert_image_vectors(rows)
+    _bump_version(user_id)
+    return [{"chunk_id": row.chunk_id, "metadata": row.meta} for row in rows]
+
+
+__all__ = ["index_text_nodes", "index_image_nodes", "embed_query_for_images", "get_index_version"]

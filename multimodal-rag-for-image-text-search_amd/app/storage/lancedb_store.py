@@ -1,0 +1,183 @@
+"""Drop-in for the reference's ``app/storage/lancedb_store.py`` backed by the GPU index.
+
+Same names and signatures: ``VectorRow`` (:12-21), ``LanceDBStore(db_path)`` (:24)
+with ``upsert_text_vectors`` / ``upsert_image_vectors`` (:87-101), ``search_text`` /
+``search_image`` (:103-123) and the static helpers ``_normalize`` (:63-69),
+``_prepare_rows`` (:71-85), ``_format_results`` (:125-139), ``_where_clause`` (:141-144).
+
+What changes underneath: the two Lance tables (text_collection / image_collection)
+become ``app.vector_store.FlatIndex`` objects resident in HBM; the ``user_id`` filter
+becomes an int32 row label (prefilter); a per-row delete becomes a tombstone label.
+Every ``LanceDBStore`` opened on the same directory shares the same tables (the
+reference's two handles on one directory could miss each other's writes).
+Semantics pinned in DESIGN.md §3: exact flat cosine (no IVF_PQ — the reference's
+index build is attempted on an empty table and swallowed, :51-60), prefilter, order
+(score desc, row asc), ``limit(max(top_k, 1))``, ``score = 1 - f32(1 - cos)``.
+"""
+from __future__ import annotations
+
+import json
+import os
+import threading
+from dataclasses import dataclass
+from typing import Any, Dict, Iterable, List, Optional, Sequence
+
+import numpy as np
+
+
+@dataclass
+class VectorRow:
+    """Payload used when writing vectors (same fields as the reference)."""
+
+    chunk_id: str
+    user_id: str
+    document_id: str
+    modality: str
+    embedding: Sequence[float]
+    meta: Dict[str, Any]
+
+
+class _Table:
+    """One collection: GPU rows + host-side row payloads."""
+
+    def __init__(self, name: str, device: int = 0):
+        self.name = name
+        self.device = device
+        self.index = None  # FlatIndex, created on the first write (dim unknown before)
+        self.dim: Optional[int] = None
+        self.chunk_ids: List[str] = []
+        self.metas: List[str] = []
+        self.doc_ids: List[str] = []
+        self.by_chunk: Dict[str, List[int]] = {}
+        self.labels: Dict[str, int] = {}
+        self.lock = threading.RLock()
+
+    def _ensure_index(self, dim: int):
+        if self.index is None:
+            from app.vector_store import FlatIndex
+
+            self.index = FlatIndex(dim, device=self.device)
+            self.dim = dim
+        elif dim != self.dim:
+            raise ValueError(f"{self.name}: embedding dim {dim} != table dim {self.dim}")
+
+    def upsert(self, payloads: List[Dict[str, Any]]) -> None:
+        if not payloads:
+            return
+        with self.lock:
+            emb = np.asarray([p["embedding"] for p in payloads], dtype=np.float32)
+            if emb.ndim != 2:
+                raise ValueError("all embeddings in one upsert must have the same length")
+            self._ensure_index(emb.shape[1])
+            # per-row delete of any existing row with the same chunk_id (lancedb_store.py:91-92)
+            dead = []
+            for p in payloads:
+                dead.extend(self.by_chunk.pop(p["chunk_id"], []))
+            if dead:
+                self.index.delete(dead)
+            labs = np.asarray([self.labels.setdefault(p["user_id"], len(self.labels)) for p in payloads],
+                              dtype=np.int32)
+            first = self.index.add(emb, labs)
+            for i, p in enumerate(payloads):
+                self.chunk_ids.append(p["chunk_id"])
+                self.metas.append(p["meta"])
+                self.doc_ids.append(p["document_id"])
+                self.by_chunk.setdefault(p["chunk_id"], []).append(first + i)
+
+    def search(self, user_id: str, vector: List[float], k: int) -> List[Dict[str, Any]]:
+        with self.lock:
+            label = self.labels.get(user_id)
+            if self.index is None or label is None:
+                return []
+            q = np.asarray(vector, dtype=np.float32)[None, :]
+            if q.shape[1] != self.dim:
+                raise ValueError(f"{self.name}: query dim {q.shape[1]} != table dim {self.dim}")
+            s, r = self.index.search(q, k, label=label)
+            rows = []
+            for score, row in zip(s[0], r[0]):
+                if row < 0:
+                    break
+                rows.append({
+                    "chunk_id": self.chunk_ids[row],
+                    "_distance": np.float32(1.0) - np.float32(score),  # lance: f32 cosine distance
+                    "meta": self.metas[row],
+                })
+            return rows
+
+
+_REGISTRY: Dict[str, Dict[str, _Table]] = {}
+_REG_LOCK = threading.Lock()
+
+
+def _tables_for(db_path: str) -> Dict[str, _Table]:
+    key = os.path.abspath(db_path)
+    with _REG_LOCK:
+        if key not in _REGISTRY:
+            dev = int(os.environ.get("MRAG_DEVICE", "0"))
+            _REGISTRY[key] = {n: _Table(n, dev) for n in ("text_collection", "image_collection")}
+        return _REGISTRY[key]
+
+
+class LanceDBStore:
+    """Two collections (text / image) with exact cosine search on the GPU."""
+
+    def __init__(self, db_path: str) -> None:
+        self._db_path = db_path
+        tables = _tables_for(db_path)
+        self._text_table = tables["text_collection"]
+        self._image_table = tables["image_collection"]
+
+    @staticmethod
+    def _normalize(vector: Sequence[float]) -> List[float]:
+        arr = np.asarray(vector, dtype=np.float32)
+        norm = np.linalg.norm(arr)
+        if norm <= 0:
+            return arr.tolist()
+        return (arr / norm).tolist()
+
+    @staticmethod
+    def _prepare_rows(rows: Iterable[VectorRow]) -> List[Dict[str, Any]]:
+        return [
+            {
+                "chunk_id": row.chunk_id,
+                "user_id": row.user_id,
+                "document_id": row.document_id,
+                "modality": row.modality,
+                "embedding": LanceDBStore._normalize(row.embedding),
+                "meta": json.dumps(row.meta or {}),
+            }
+            for row in rows
+        ]
+
+    def upsert_text_vectors(self, rows: Iterable[VectorRow]) -> None:
+        self._text_table.upsert(self._prepare_rows(rows))
+
+    def upsert_image_vectors(self, rows: Iterable[VectorRow]) -> None:
+        self._image_table.upsert(self._prepare_rows(rows))
+
+    def search_text(self, user_id: str, query_vec: Sequence[float], top_k: int) -> List[Dict[str, Any]]:
+        return self._format_results(self._text_table.search(user_id, self._normalize(query_vec), max(top_k, 1)))
+
+    def search_image(self, user_id: str, query_vec: Sequence[float], top_k: int) -> List[Dict[str, Any]]:
+        return self._format_results(self._image_table.search(user_id, self._normalize(query_vec), max(top_k, 1)))
+
+    @staticmethod
+    def _format_results(rows: List[Dict[str, Any]]) -> List[Dict[str, Any]]:
+        out = [
+            {
+                "chunk_id": row.get("chunk_id"),
+                "score": 1.0 - float(row.get("_distance", 0.0)),
+                "meta": json.loads(row.get("meta") or "{}"),
+            }
+            for row in rows
+        ]
+        out.sort(key=lambda item: item["score"], reverse=True)
+        return out
+
+    @staticmethod
+    def _where_clause(column: str, value: str) -> str:
+        safe = str(value).replace("'", "''")
+        return f"{column} == '{safe}'"
+
+
+__all__ = ["VectorRow", "LanceDBStore"]

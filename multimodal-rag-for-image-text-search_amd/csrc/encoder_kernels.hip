@@ -363,9 +363,18 @@ int launch_attention(const AttentionArgs& a, int dh, hipStream_t s) {
   if (a.B <= 0) return MRAG_OK;
   MRAG_REQUIRE(a.L >= 1 && a.L <= 256, "attention: L=%d unsupported (1..256)", a.L);
   const size_t shm = (size_t)2 * a.L * dh * 4 + (size_t)a.L * 4;
-  MRAG_REQUIRE(shm <= 65536, "attention: L*dh too large for LDS");
+  MRAG_REQUIRE(shm <= 160 * 1024, "attention: L*dh too large for LDS");
   const int threads = (a.L + 63) / 64 * 64;
   const dim3 grid((unsigned)(a.B * a.H));
+  // K/V of a head stay f32 in LDS; above 64 KiB the kernel must opt in (gfx950: 160 KiB/CU)
+  static bool attr_set = false;
+  if (!attr_set) {
+    MRAG_HIP(hipFuncSetAttribute((const void*)attention_kernel<64>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 160 * 1024));
+    MRAG_HIP(hipFuncSetAttribute((const void*)attention_kernel<32>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 160 * 1024));
+    attr_set = true;
+  }
   if (dh == 64) {
     hipLaunchKernelGGL(attention_kernel<64>, grid, dim3(threads), shm, s, a);
   } else if (dh == 32) {

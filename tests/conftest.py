@@ -8,8 +8,12 @@ from __future__ import annotations
 
 import os
 import sys
+import tempfile
 
 import pytest
+
+# the compat layer reads LANCEDB_DIR at import time (as the reference's settings do)
+os.environ.setdefault("LANCEDB_DIR", tempfile.mkdtemp(prefix="mrag_lancedb_"))
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "multimodal-rag-for-image-text-search_amd")

@@ -1,0 +1,138 @@
+"""End-to-end parity of the drop-in API on the GPU engine.
+
+* LanceDBStore.upsert_*/search_* vs the exact oracle (user prefilter, upsert-replaces,
+  score = 1 - f32(1 - cos) like lance's f32 distance, limit max(k, 1));
+* embed_images_batch(paths) on the reference's PNG files vs the reference's own
+  embed_images_batch output for the same files (golden), tolerance as the encoders;
+* index_text_nodes -> retrieve_text / retrieve_images / retrieve, and the batched
+  app.retrieval path, against the oracle over the stored vectors.
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import pytest
+from PIL import Image
+
+from conftest import GOLDEN
+from _data import unit_rows
+from oracle.knn import flat_cosine_topk
+from oracle.normalize import store_normalize
+
+pytestmark = pytest.mark.gpu
+
+
+def _ref_score(s64: float) -> float:
+    return 1.0 - float(np.float32(1.0) - np.float32(s64))
+
+
+def test_store_vs_oracle(cuda, tmp_path):
+    from app.storage.lancedb_store import LanceDBStore, VectorRow
+
+    store = LanceDBStore(str(tmp_path / "db"))
+    rng = np.random.default_rng(0)
+    X = unit_rows(3000, 384, 5) * 2.0
+    users = rng.integers(0, 3, len(X))
+    rows = [VectorRow(chunk_id=f"c{i}", user_id=f"u{users[i]}", document_id="d", modality="text",
+                      embedding=X[i].tolist(), meta={"i": i}) for i in range(len(X))]
+    store.upsert_text_vectors(rows[:2000])
+    store.upsert_text_vectors(rows[2000:])
+    # re-upsert 100 chunk ids with new vectors: old rows must disappear
+    Y = unit_rows(100, 384, 6)
+    store.upsert_text_vectors([VectorRow(chunk_id=f"c{i}", user_id=f"u{users[i]}", document_id="d",
+                                         modality="text", embedding=Y[i].tolist(), meta={"i": i, "v": 2})
+                               for i in range(100)])
+    stored = np.asarray([store_normalize(x) for x in X], np.float32)
+    stored[:100] = np.asarray([store_normalize(y) for y in Y], np.float32)
+    q = unit_rows(5, 384, 7)
+    for u in range(3):
+        lab = (users == u).astype(np.int64) - 1  # 0 for this user, -1 otherwise
+        lab[lab < 0] = -2
+        for k in (1, 10, 50):
+            os_, or_ = flat_cosine_topk(stored, lab, np.asarray([store_normalize(v) for v in q], np.float32), k,
+                                        label_filter=0)
+            for qi in range(len(q)):
+                got = store.search_text(f"u{u}", q[qi].tolist(), k)
+                assert [g["chunk_id"] for g in got] == [f"c{r}" for r in or_[qi] if r >= 0]
+                assert [g["score"] for g in got] == pytest.approx([_ref_score(s) for s in os_[qi] if s > -np.inf],
+                                                                  abs=1e-6)
+        assert store.search_text(f"u{u}", q[0].tolist(), 0)  # limit(max(k, 1))
+    assert store.search_text("nobody", q[0].tolist(), 5) == []
+    assert store.search_image("u0", np.ones(512).tolist(), 5) == []
+
+
+def test_embed_images_batch_matches_reference_output(cuda, tmp_path):
+    from app.ml import embeddings
+
+    g = np.load(os.path.join(GOLDEN, "golden_clip_image.npz"))
+    imgs = [g["raw_0"], g["images_u8"][1], g["raw_2"]]
+    paths = []
+    for i, a in enumerate(imgs):
+        p = tmp_path / f"img{i}.png"
+        Image.fromarray(a).save(p)
+        paths.append(p)
+    got = embeddings.embed_images_batch(paths)
+    exp = g["expected"]
+    cos = np.sum(got * exp, 1) / (np.linalg.norm(got, axis=1) * np.linalg.norm(exp, axis=1))
+    assert got.shape == (3, 512) and cos.min() >= 0.9995 and np.abs(got - exp).max() <= 1.5e-2
+    assert np.allclose(np.linalg.norm(got, axis=1), 1.0, atol=1e-6)
+
+
+def test_index_retrieve_end_to_end(cuda, tmp_path, monkeypatch):
+    from app.cache import clear_all_caches
+    from app.ml import embeddings, index_build, retrieve
+    from app.retrieval import retrieve_batch
+    from app.storage.lancedb_store import LanceDBStore
+    from app.storage.schema import Chunk, MetadataStore
+
+    store = LanceDBStore(str(tmp_path / "db2"))
+    meta = MetadataStore(str(tmp_path / "db2" / "metadata.sqlite3"))
+    monkeypatch.setattr(index_build, "_LANCEDB_STORE", store)
+    monkeypatch.setattr(index_build, "_VERSION_FILE", tmp_path / "versions.json")
+    monkeypatch.setattr(retrieve, "_LANCEDB_STORE", store)
+    monkeypatch.setattr(retrieve, "_METADATA_STORE", meta)
+    monkeypatch.setattr(retrieve, "get_index_version", index_build.get_index_version)
+    clear_all_caches()
+    rng = np.random.default_rng(1)
+    words = [f"w{i}" for i in range(400)]
+    nodes = [{"id": f"doc{d}", "text": " ".join(" ".join(rng.choice(words, 12)) + "." for _ in range(40)),
+              "metadata": {"source": "pdf", "page_no": d}} for d in range(6)]
+    stored = index_build.index_text_nodes("alice", nodes)
+    index_build.index_text_nodes("bob", nodes[:2])
+    meta.upsert_chunks([Chunk(id=s["chunk_id"], document_id=s["metadata"]["doc_id"], modality="text", text=s["text"],
+                              meta=s["metadata"]) for s in stored])
+    # image side: 5 images for alice
+    ipaths = []
+    for i in range(5):
+        p = tmp_path / f"im{i}.png"
+        Image.fromarray(rng.integers(0, 256, (64 + 10 * i, 80, 3), dtype=np.uint8)).save(p)
+        ipaths.append(p)
+    inodes = [{"id": f"img{i}", "metadata": {"file_path": str(p), "doc_id": "docimg"}} for i, p in enumerate(ipaths)]
+    index_build.index_image_nodes("alice", inodes)
+    meta.upsert_chunks([Chunk(id=f"img{i}", document_id="docimg", modality="image", file_path=str(p))
+                        for i, p in enumerate(ipaths)])
+    assert index_build.get_index_version("alice") == 2
+
+    # oracle over exactly the vectors that were stored
+    texts = [n.get_content("all") for n in index_build._SPLITTER.get_nodes_from_documents(
+        [index_build.Document(text=n["text"], metadata=n["metadata"], doc_id=n["id"]) for n in nodes])]
+    tvecs = np.asarray([store_normalize(v) for v in embeddings.embed_text_batch(texts)], np.float32)
+    ids = [s["chunk_id"] for s in stored]
+    queries = ["w1 w2 w3 w4 w5", "w300 w12", "w7"]
+    for qtext in queries:
+        res = retrieve.retrieve_text("alice", qtext, top_k=7)
+        qv = np.asarray(store_normalize(embeddings.embed_text_batch([qtext])[0]), np.float32)
+        _, orr = flat_cosine_topk(tvecs, np.zeros(len(tvecs)), qv, 7)
+        assert [r["chunk_id"] for r in res] == [ids[r] for r in orr[0] if r >= 0]
+        assert all(r["modality"] == "text" and r["text"] for r in res)
+        imgs = retrieve.retrieve_images("alice", qtext)
+        assert sorted(r["chunk_id"] for r in imgs) == [f"img{i}" for i in range(5)]
+        assert [r["score"] for r in imgs] == sorted([r["score"] for r in imgs], reverse=True)
+    clear_all_caches()
+    single = [retrieve._fuse_results(retrieve.retrieve_text("alice", q), retrieve.retrieve_images("alice", q))
+              for q in queries]
+    batched = retrieve_batch("alice", queries)
+    for a, b in zip(single, batched):
+        assert [x["chunk_id"] for x in a] == [x["chunk_id"] for x in b]
+        assert [x["combined_score"] for x in a] == pytest.approx([x["combined_score"] for x in b], abs=1e-5)

@@ -106,3 +106,17 @@ def test_minilm_golden(cuda):
     enc = GpuEncoder(MINILM_L6)
     _cmp(enc.embed_tokens(g["ids"], g["mask"]), g["expected"])
     _cmp(enc.embed_tokens(g["ids"], g["mask"], normalize=False), g["expected_unnormalized"], unit=False)
+
+
+def test_minilm_max_length_256(cuda):
+    """ST max_seq_length 256: the longest sequence the reference feeds MiniLM."""
+    from app.encoders import MINILM_L6, GpuEncoder
+    from oracle.models import bert_model, minilm_embeds
+
+    rng = np.random.default_rng(5)
+    ids = rng.integers(1000, 30000, (3, 256)).astype(np.int32)
+    ids[:, 0], ids[:, -1] = 101, 102
+    mask = np.ones_like(ids)
+    mask[1, 200:] = 0
+    enc = GpuEncoder(MINILM_L6)
+    _cmp(enc.embed_tokens(ids, mask), minilm_embeds(bert_model(0), ids, mask))
