@@ -1,0 +1,9 @@
+#!/bin/bash
+# Bench + rocprofv3 kernel trace/stats + PMC passes (FETCH_SIZE, WRITE_SIZE) for profiles/.
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd $R
+timeout -k 10 400 python bench.py > gpurun_out/bench_full.log 2>&1 || { echo "bench failed rc=$?" >> gpurun_out/bench_full.log; exit 1; }
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_stats -o run -- python3 $R/bench.py --steps 20 --warmup 3 --no-cpu-baseline > $R/gpurun_out/prof_stats.log 2>&1 || exit 2
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $R/gpurun_out/prof_fetch -o run -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-clip > $R/gpurun_out/prof_fetch.log 2>&1 || exit 3
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $R/gpurun_out/prof_write -o run -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-clip > $R/gpurun_out/prof_write.log 2>&1 || exit 4
