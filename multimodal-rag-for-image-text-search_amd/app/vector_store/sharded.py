@@ -1,0 +1,59 @@
+"""Row-sharded flat index over one node's GPUs (BASELINE config 4).
+
+One process per GPU (torch.distributed, backend "nccl" = RCCL over xGMI). Rank r owns
+the contiguous global rows [row_offset_r, row_offset_r + n_r) in its own
+``FlatIndex``. A search is:
+
+  1. local exact top-k on every rank (K7/K8/K10; global row ids via row_offset);
+  2. ONE all-gather of the per-shard (f64 score, int64 row) lists, [world, nq, k]
+     (1000 x 10 x 16 B = 160 KB per rank: latency-bound, far below the scan time);
+  3. the K11 merge under (score desc, row asc) — identical to a single-index search
+     because every shard's list is its exact top-k.
+
+No other collective exists on the data path; queries are replicated (every rank gets
+the same batch), results are replicated on every rank.
+"""
+from __future__ import annotations
+
+from typing import Callable, Optional, Tuple
+
+
+class ShardedFlatIndex:
+    def __init__(self, local_index, row_offset: int, group=None,
+                 merge: Optional[Callable] = None):
+        import torch.distributed as dist
+
+        self.local = local_index
+        self.row_offset = int(row_offset)
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        if merge is None:
+            from app.vector_store import topk_merge
+
+            merge = topk_merge
+        self._merge = merge
+        self._buf = None
+
+    def _gather(self, t):
+        import torch
+        import torch.distributed as dist
+
+        shape = (self.world,) + tuple(t.shape)
+        if dist.get_backend(self.group) == "nccl":
+            out = torch.empty(shape, dtype=t.dtype, device=t.device)
+            dist.all_gather_into_tensor(out, t.contiguous(), group=self.group)
+            return out
+        parts = [torch.empty_like(t) for _ in range(self.world)]
+        dist.all_gather(parts, t.contiguous(), group=self.group)
+        return torch.stack(parts)
+
+    def search(self, queries, k: int, label: int = -1) -> Tuple:
+        """(scores f32 [nq,k], rows int64 [nq,k]) over the whole sharded corpus."""
+        s, r, s64 = self.local.search(queries, k, label=label, row_offset=self.row_offset, with_f64=True)
+        if self.world == 1:
+            return s, r
+        ms, mr, _ = self._merge(self._gather(s64), self._gather(r), k)
+        return ms, mr
+
+
+__all__ = ["ShardedFlatIndex"]
