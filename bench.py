@@ -273,6 +273,7 @@ def main():
             out["cpu_baseline"] = cpu_baseline()
         print(json.dumps(out), flush=True)
     if world > 1:
+        dist.barrier()  # ranks > 0 wait while rank 0 runs the single-GPU CLIP leg
         dist.destroy_process_group()
 
 
