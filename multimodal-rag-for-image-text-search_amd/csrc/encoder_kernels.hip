@@ -10,6 +10,8 @@
 // Layout: activations row-major [tokens][features]; the residual stream is f32, every GEMM
 // input is f16 (LayerNorm writes the f16 copy), weights are f16 [out][in] (torch Linear
 // layout, K contiguous for both GEMM operands), biases / LN params / embeddings f32.
+#include <cstdlib>
+
 #include "common.h"
 #include "encoder_kernels.h"
 
@@ -84,19 +86,26 @@ __global__ __launch_bounds__(GTHREADS) void gemm_nt_kernel(GemmArgs g) {
     if (ks + 1 < ksteps) stage(cur ^ 1, (ks + 1) * GK);
     const char* At = (const char*)smem + cur * STAGE_BYTES;
     const char* Bt = At + GM * GK * 2;
+    // read all 16 fragments of this 64-deep step first (64 VGPRs), then 16 MFMAs: the LDS
+    // latency of later sub-steps hides under the earlier MFMAs
+    half8 a[GK / 16][2], b[GK / 16][2];
 #pragma unroll
     for (int kk = 0; kk < GK / 16; ++kk) {
       const int coff = (((2 * kk + h) ^ sw) * 16);
-      half8 a[2], b[2];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) a[i] = *(const half8*)(At + (wr * 64 + i * 32 + r32) * 128 + coff);
+      for (int i = 0; i < 2; ++i) a[kk][i] = *(const half8*)(At + (wr * 64 + i * 32 + r32) * 128 + coff);
 #pragma unroll
-      for (int j = 0; j < 2; ++j) b[j] = *(const half8*)(Bt + (wc * 64 + j * 32 + r32) * 128 + coff);
+      for (int j = 0; j < 2; ++j) b[kk][j] = *(const half8*)(Bt + (wc * 64 + j * 32 + r32) * 128 + coff);
+    }
+    __builtin_amdgcn_sched_barrier(0);  // keep the reads ahead (hipcc would re-interleave them)
+#pragma unroll
+    for (int kk = 0; kk < GK / 16; ++kk)
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[i], b[j], acc[i][j], 0, 0, 0);
-    }
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[kk][i], b[kk][j], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);  // MFMAs stay ahead of the stage wait + barrier
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
@@ -225,6 +234,136 @@ __global__ __launch_bounds__(256) void attention_kernel(AttentionArgs a) {
   _Float16* orow = a.out + ((size_t)b * a.L + i) * D + hd * DH;
 #pragma unroll
   for (int d = 0; d < DH; ++d) orow[d] = (_Float16)(o[d] * inv);
+}
+
+// K4 (MFMA form) for L <= 64, head_dim 64 — the ViT-B/32 case (L = 50) and short text.
+// One wave per (sequence, head), 4 heads per workgroup. Sequence padded to 64.
+//   S^T = K . Q^T   (4 x 2x2 MFMA 32x32x16): lane owns query q = (l&31) + 32*qb, registers
+//                   hold keys (reg&3) + 8(reg>>2) + 4(l>>5) + 32*kb, so the row softmax over
+//                   keys is in-register plus one xor-32 shuffle (guide T12 "swapped QK^T").
+//   O   = P . V     (4 x 2x2 MFMA): the P accumulator registers 8t..8t+7 of key block kb are
+//                   the A fragment of k-step s = 2kb + t with the k order permuted
+//                   (element j <-> key 16s + 8(j>>2) + 4(l>>5) + (j&3); guide §3
+//                   "An accumulator tile as the next MFMA's operand"); V is gathered from
+//                   LDS in that same order. P is normalised by its row sum before the cast.
+__global__ __launch_bounds__(256) void attention_mfma64_kernel(AttentionArgs a) {
+  constexpr int DH = 64;
+  __shared__ __attribute__((aligned(16))) _Float16 Vs[4][64][DH];  // per-wave V tile (8 KiB)
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  const int hh = lane >> 5, r = lane & 31;
+  const int pair = blockIdx.x * 4 + w;
+  const bool active = pair < a.B * a.H;
+  const int b = active ? pair / a.H : 0, hd = active ? pair - (pair / a.H) * a.H : 0;
+  const int D = a.H * DH, L = a.L;
+  const size_t rs = (size_t)3 * D;
+  const _Float16* base = a.qkv + (size_t)b * L * rs;
+
+  // V tile -> LDS (row per lane, zero rows >= L)
+  {
+    const int key = lane;
+    half8* dst = (half8*)&Vs[w][key][0];
+    if (active && key < L) {
+      const half8* src = (const half8*)(base + (size_t)key * rs + 2 * D + hd * DH);
+#pragma unroll
+      for (int c = 0; c < 8; ++c) dst[c] = src[c];
+    } else {
+#pragma unroll
+      for (int c = 0; c < 8; ++c) dst[c] = half8{};
+    }
+  }
+  // K (A operand) and Q (B operand) fragments: row r + 32*blk, dims 16s + 8hh .. +7
+  half8 kf[2][4], qf[2][4];
+#pragma unroll
+  for (int blk = 0; blk < 2; ++blk) {
+    const int row = r + 32 * blk;
+    const bool ok = active && row < L;
+    const _Float16* kr = base + (size_t)row * rs + D + hd * DH + 8 * hh;
+    const _Float16* qr = base + (size_t)row * rs + hd * DH + 8 * hh;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      kf[blk][s] = ok ? *(const half8*)(kr + 16 * s) : half8{};
+      qf[blk][s] = ok ? *(const half8*)(qr + 16 * s) : half8{};
+    }
+  }
+  __syncthreads();
+  if (!active) return;
+
+  f32x16 st[2][2];  // [key block][query block]
+#pragma unroll
+  for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) {
+      f32x16 acc = {};
+#pragma unroll
+      for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf[kb][s], qf[qb][s], acc, 0, 0, 0);
+      st[kb][qb] = acc;
+    }
+
+  // softmax over keys for the lane's two queries
+  half8 pa[2][4];  // [query block][k-step]
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    const int q = r + 32 * qb;
+    float m = -INFINITY;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) {
+        const int key = (reg & 3) + 8 * (reg >> 2) + 4 * hh + 32 * kb;
+        bool ok = key < L;
+        if (a.mask) ok = ok && a.mask[(size_t)b * L + min(key, L - 1)] != 0;
+        if (a.causal) ok = ok && key <= q;
+        const float v = ok ? st[kb][qb][reg] * a.scale : -INFINITY;
+        st[kb][qb][reg] = v;
+        m = fmaxf(m, v);
+      }
+    m = fmaxf(m, __shfl_xor(m, 32));
+    float l = 0.f;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) {
+        const float pv = m == -INFINITY ? 0.f : __expf(st[kb][qb][reg] - m);
+        st[kb][qb][reg] = pv;
+        l += pv;
+      }
+    l += __shfl_xor(l, 32);
+    const float inv = l > 0.f ? 1.f / l : 0.f;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int kb = s >> 1, t = s & 1;
+      half8 f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] = (_Float16)(st[kb][qb][8 * t + j] * inv);
+      pa[qb][s] = f;
+    }
+  }
+  // V fragments in the permuted key order: element j <-> key 16s + 8(j>>2) + 4hh + (j&3)
+  half8 vf[2][4];  // [dim block][k-step]
+#pragma unroll
+  for (int db = 0; db < 2; ++db)
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      half8 f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] = Vs[w][16 * s + 8 * (j >> 2) + 4 * hh + (j & 3)][r + 32 * db];
+      vf[db][s] = f;
+    }
+  _Float16* orow = a.out + (size_t)b * L * D + hd * DH;
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+    for (int db = 0; db < 2; ++db) {
+      f32x16 acc = {};
+#pragma unroll
+      for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(pa[qb][s], vf[db][s], acc, 0, 0, 0);
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) {
+        const int q = (reg & 3) + 8 * (reg >> 2) + 4 * hh + 32 * qb;
+        if (q < L) orow[(size_t)q * D + r + 32 * db] = (_Float16)acc[reg];
+      }
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -359,6 +498,15 @@ int launch_layernorm(const LayerNormArgs& a, hipStream_t s) {
   return MRAG_OK;
 }
 
+// MRAG_ATTN_VALU=1 forces the VALU form everywhere (cross-check in tests).
+bool force_valu_attention() {
+  static const bool v = [] {
+    const char* e = getenv("MRAG_ATTN_VALU");
+    return e && atoi(e) == 1;
+  }();
+  return v;
+}
+
 int launch_attention(const AttentionArgs& a, int dh, hipStream_t s) {
   if (a.B <= 0) return MRAG_OK;
   MRAG_REQUIRE(a.L >= 1 && a.L <= 256, "attention: L=%d unsupported (1..256)", a.L);
@@ -375,7 +523,9 @@ int launch_attention(const AttentionArgs& a, int dh, hipStream_t s) {
                                  160 * 1024));
     attr_set = true;
   }
-  if (dh == 64) {
+  if (dh == 64 && a.L <= 64 && !force_valu_attention()) {
+    hipLaunchKernelGGL(attention_mfma64_kernel, dim3((unsigned)((a.B * a.H + 3) / 4)), dim3(256), 0, s, a);
+  } else if (dh == 64) {
     hipLaunchKernelGGL(attention_kernel<64>, grid, dim3(threads), shm, s, a);
   } else if (dh == 32) {
     hipLaunchKernelGGL(attention_kernel<32>, grid, dim3(threads), shm, s, a);

@@ -72,14 +72,106 @@ __device__ float pw_sumsq(const float* __restrict__ x, int n) {
   return val[0];
 }
 
+// numpy's recursion splits n > 128 at n2 = (n/2) - (n/2)%8, so for 128 < n <= 1024 the
+// leaves are 2..8 blocks of 64..128 elements for n <= 968 (checked on the host for every n);
+// n <= 128 is a single leaf.
+struct Leaves {
+  int n;
+  int off[8], len[8];
+};
+
+__device__ void leaves_of(int off, int n, Leaves& L) {
+  if (n <= 128) {
+    L.off[L.n] = off;
+    L.len[L.n] = n;
+    ++L.n;
+    return;
+  }
+  int n2 = n / 2;
+  n2 -= n2 % 8;
+  // depth <= 3 for n <= 1024: unrolled recursion through a tiny explicit stack
+  int so[8], sn[8], sp = 0;
+  so[sp] = off + n2; sn[sp++] = n - n2;
+  so[sp] = off; sn[sp++] = n2;
+  while (sp) {
+    const int o = so[--sp], m = sn[sp];
+    if (m <= 128) {
+      L.off[L.n] = o;
+      L.len[L.n] = m;
+      ++L.n;
+    } else {
+      int h = m / 2;
+      h -= h % 8;
+      so[sp] = o + h; sn[sp++] = m - h;
+      so[sp] = o; sn[sp++] = h;
+    }
+  }
+}
+
+// Tree combination of the leaf sums in numpy's order: (left + right) recursively.
+__device__ float combine(const float* leaf, int off, int n, int& li) {
+  if (n <= 128) return leaf[li++];
+  int n2 = n / 2;
+  n2 -= n2 % 8;
+  const float a = combine(leaf, off, n2, li);
+  const float b = combine(leaf, off + n2, n - n2, li);
+  return __fadd_rn(a, b);
+}
+
+// One wave per row. Lane 8*leaf + j owns accumulator j of leaf `leaf` (numpy keeps 8
+// strided accumulators per leaf); leaf and tree combinations follow numpy's order exactly.
+__global__ __launch_bounds__(256) void l2norm_rows_wave_kernel(const float* x, float* y,  // may alias
+                                                               int64_t rows, int dim) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= rows) return;
+  const float* xr = x + r * dim;
+  float* yr = y + r * dim;
+  Leaves L;
+  L.n = 0;
+  leaves_of(0, dim, L);
+  const int leaf = lane >> 3, j = lane & 7;
+  float acc = 0.f;
+  if (leaf < L.n && L.len[leaf] >= 8) {
+    const float* p = xr + L.off[leaf];
+    const int full = L.len[leaf] - L.len[leaf] % 8;
+    acc = __fmul_rn(p[j], p[j]);
+    for (int i = j + 8; i < full; i += 8) acc = __fadd_rn(acc, __fmul_rn(p[i], p[i]));
+  }
+  // leaf value on lane 8*leaf: ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)) then the tail in order
+  const int b = lane & ~7;
+  const float r0 = __shfl(acc, b + 0), r1 = __shfl(acc, b + 1), r2 = __shfl(acc, b + 2), r3 = __shfl(acc, b + 3);
+  const float r4 = __shfl(acc, b + 4), r5 = __shfl(acc, b + 5), r6 = __shfl(acc, b + 6), r7 = __shfl(acc, b + 7);
+  float lv = 0.f;
+  if (j == 0 && leaf < L.n) {
+    const float* p = xr + L.off[leaf];
+    const int n = L.len[leaf];
+    if (n < 8) {
+      lv = -0.0f;
+      for (int i = 0; i < n; ++i) lv = __fadd_rn(lv, __fmul_rn(p[i], p[i]));
+    } else {
+      lv = __fadd_rn(__fadd_rn(__fadd_rn(r0, r1), __fadd_rn(r2, r3)), __fadd_rn(__fadd_rn(r4, r5), __fadd_rn(r6, r7)));
+      for (int i = n - n % 8; i < n; ++i) lv = __fadd_rn(lv, __fmul_rn(p[i], p[i]));
+    }
+  }
+  float leafv[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) leafv[q] = __shfl(lv, 8 * q);
+  int li = 0;
+  const float ss = combine(leafv, 0, dim, li);
+  // v_sqrt_f32 is 1-ulp; sqrt and division are evaluated in f64 and rounded once
+  // to f32, which is the correctly rounded f32 result (53 >= 2*24 + 2).
+  float nrm = (float)sqrt((double)ss);
+  if (nrm == 0.0f) nrm = 1.0f;
+  for (int d = lane; d < dim; d += 64) yr[d] = (float)((double)xr[d] / (double)nrm);
+}
+
 __global__ void l2norm_rows_kernel(const float* x, float* y,  // may alias
                                    int64_t rows, int dim) {
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= rows) return;
   const float* xr = x + r * dim;
   float* yr = y + r * dim;
-  // v_sqrt_f32 is 1-ulp; sqrt and division are evaluated in f64 and rounded once
-  // to f32, which is the correctly rounded f32 result (53 >= 2*24 + 2).
   float nrm = (float)sqrt((double)pw_sumsq(xr, dim));
   if (nrm == 0.0f) nrm = 1.0f;
   for (int d = 0; d < dim; ++d) yr[d] = (float)((double)xr[d] / (double)nrm);
@@ -93,11 +185,18 @@ extern "C" int mrag_l2norm_rows(const float* x, float* y, int64_t rows, int32_t 
   MRAG_REQUIRE(dim <= (1 << 20), "dim %d too large", dim);
   if (rows == 0) return MRAG_OK;
   MRAG_REQUIRE(x != nullptr && y != nullptr, "NULL pointer");
-  const int threads = 64;
-  const int64_t blocks = (rows + threads - 1) / threads;
-  MRAG_REQUIRE(blocks < (1ll << 31), "too many rows");
-  hipLaunchKernelGGL(l2norm_rows_kernel, dim3((unsigned)blocks), dim3(threads), 0,
-                     (hipStream_t)stream, x, y, rows, (int)dim);
+  if (dim <= 968) {  // wave per row: numpy splits dims <= 968 into <= 8 leaves of <= 128
+    const int64_t blocks = (rows + 3) / 4;
+    MRAG_REQUIRE(blocks < (1ll << 31), "too many rows");
+    hipLaunchKernelGGL(l2norm_rows_wave_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, x, y,
+                       rows, (int)dim);
+  } else {  // thread per row, generic recursion
+    const int threads = 64;
+    const int64_t blocks = (rows + threads - 1) / threads;
+    MRAG_REQUIRE(blocks < (1ll << 31), "too many rows");
+    hipLaunchKernelGGL(l2norm_rows_kernel, dim3((unsigned)blocks), dim3(threads), 0, (hipStream_t)stream, x, y,
+                       rows, (int)dim);
+  }
   MRAG_CHECK_LAUNCH();
   return MRAG_OK;
 }

@@ -153,7 +153,7 @@ def test_l2norm_bit_exact(cuda):
     from app.vector_store import l2norm_rows
 
     rng = np.random.default_rng(0)
-    for d in (384, 512, 7, 300):
+    for d in (384, 512, 7, 300, 129, 968, 969, 1000, 128, 64):
         x = (rng.standard_normal((257, d)) * rng.uniform(0.01, 50, (257, 1))).astype(np.float32)
         x[3] = 0.0
         ref = x / np.where(np.linalg.norm(x, axis=1, keepdims=True) == 0, 1.0,
