@@ -28,6 +28,8 @@
 #include <algorithm>
 #include <cstdlib>
 #include <mutex>
+#include <type_traits>
+#include <utility>
 #include <vector>
 
 #include "common.h"
@@ -69,6 +71,8 @@ struct ScanParams {
   int ccap;
   // shared per-query rejection threshold (ordered-uint f32, 0 == none), top-k mode
   uint32_t* theta;
+  // sample pre-pass (v2 MODE 1): tiles split + i * splits * sample_stride, i < sample_tiles
+  int sample_tiles, sample_stride;
 };
 
 template <int KL>
@@ -352,6 +356,376 @@ __global__ __launch_bounds__(SCAN_THREADS) void knn_scan_kernel(ScanParams p) {
 }
 
 // ---------------------------------------------------------------------------
+// K7 v2 (top-k mode, KL = 8): 4 waves x 64 queries per workgroup, one wave per SIMD.
+//
+// Why: in v1 every A fragment read from LDS feeds ONE MFMA (32 queries per wave, the
+// query fragments fill the 256-VGPR budget of 2 waves/SIMD), MFMAs wait on their
+// ds_reads, and the per-tile filter / list insertion (which fires in most tiles: a lane's
+// threshold is only its own list's KL-th or the best published one) runs between the
+// tile's MFMAs instead of beside them. Here:
+//  * the 64 queries' B fragments (DP/2 registers per lane: all 256 AGPRs at DP=512) live
+//    in the accumulator file for the whole launch — the MFMA takes B from AGPRs (inline
+//    asm with an "a" operand; hipcc loads them straight into a[...]) — so each A fragment
+//    feeds two MFMAs and the VGPR file is free for double-buffered accumulators;
+//  * A fragments are read two k-steps ahead into a 3-deep register ring;
+//  * the accumulators are double-buffered: while the MFMAs of tile t run, the filter of
+//    tile t-1 runs in the gaps between them (order pinned by sched_barrier). At one wave
+//    per SIMD only ~5 single-issue instructions hide behind one 32x32x16 MFMA, so each gap
+//    carries at most one job: the k-step's two A-fragment reads (gap 0), one next-tile
+//    LDS-DMA piece (gap 1), or one group test (gap 3): max of 8 of the lane's 64 scores
+//    against its threshold, one wave-uniform branch, and only on a hit the per-row list
+//    insertion of those 8 rows;
+//  * the shared threshold is seeded by the sample pre-pass (MODE 1) near the k-th best,
+//    so hits — and therefore insertions — are rare from the first tile on.
+// Semantics are identical to v1 (same lists, same shared threshold, same outputs).
+constexpr int SCAN2_WAVES = 4;
+constexpr int SCAN2_THREADS = SCAN2_WAVES * 64;
+constexpr int QPW2 = 64;  // two 32-query blocks per wave
+static_assert(SCAN2_WAVES * QPW2 == QPG, "v2 keeps the query-group size of v1");
+
+template <typename F, int... I>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+// acc += A.B with B resident in AGPRs (hipcc does not model asm: the caller guarantees
+// the MFMA->VALU distance with mfma_guard before any VALU reads `acc`).
+__device__ __forceinline__ void mfma_ab(f32x16& acc, const half8& a, const half8& b) {
+  asm volatile("v_mfma_f32_32x32x16_f16 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "a"(b));
+}
+__device__ __forceinline__ void mfma_ab0(f32x16& acc, const half8& a, const half8& b) {
+  asm volatile("v_mfma_f32_32x32x16_f16 %0, %1, %2, 0" : "=&v"(acc) : "v"(a), "a"(b));
+}
+// >= 18 wait states after the last MFMA writing these accumulators (8-pass XDL -> VALU).
+__device__ __forceinline__ void mfma_guard(f32x16 (&acc)[2][2]) {
+  asm volatile("s_nop 15\n\ts_nop 3" : "+v"(acc[0][0]), "+v"(acc[0][1]), "+v"(acc[1][0]), "+v"(acc[1][1]));
+}
+
+// ABL (timing experiments only, env MRAG_SCAN_ABLATE=10+ABL): 1 = no epilogue, 2 = fast filter
+// only, 3 = no epilogue + next-tile LDS-DMA issued 4 per k-step, 4 = no epilogue, no LDS-DMA.
+//
+// MODE 1 = the sample pre-pass: the same MFMA pipeline over a strided 1/sample_stride of each
+// split's tiles, keeping only each lane's running max (no lists, no inserts); the
+// per-(query, split, half) maxima go to part_s[(split * Qp + slot) * 2 + h] for
+// theta_init_kernel, which seeds the shared threshold with the k-th largest of them.
+template <int DP, int ABL = 0, int MODE = 0>
+__global__ __launch_bounds__(SCAN2_THREADS) void knn_scan2_kernel(ScanParams p) {
+  constexpr int KL = 8;
+  constexpr int KSTEPS = DP / 16;
+  constexpr int ROW_BYTES = DP * 2;
+  constexpr int TILE_BYTES = TILE_ROWS * ROW_BYTES;
+  constexpr int CPR = DP / 8;
+  constexpr int GLDS_PER_WAVE = TILE_BYTES / 1024 / SCAN2_WAVES;
+  static_assert(TILE_BYTES % (1024 * SCAN2_WAVES) == 0, "tile must split into 1 KiB pieces");
+  constexpr bool NO_EPI = ABL == 1 || ABL == 3 || ABL == 4;
+  constexpr bool NO_GLDS = ABL == 4;
+  static_assert(KSTEPS % GLDS_PER_WAVE == 0, "LDS-DMA pieces spread evenly over the k-steps");
+  static_assert(CPR % 16 == 0, "swizzle needs rows of a multiple of 16 chunks");
+  constexpr int NGROUPS = 8;  // group g: query block g>>2, row block (g>>1)&1, regs 8(g&1)..+8
+  static_assert(KSTEPS % NGROUPS == 0, "one group test every KSTEPS/8 k-steps");
+  constexpr int LBL_OFF = 2 * TILE_BYTES;
+  __shared__ __attribute__((aligned(16))) char smem[2 * TILE_BYTES + 2 * TILE_ROWS * 4];
+
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int h = lane >> 5;
+  const int r32 = lane & 31;
+  const uint32_t lds_base = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)((AS3 char*)smem));
+
+  int qg, split;  // same XCD-aware block mapping as v1
+  {
+    const int b = blockIdx.x;
+    if ((p.splits & 7) == 0) {
+      const int xcd = b & 7, sl = b >> 3;
+      qg = sl % p.qgroups;
+      split = (sl / p.qgroups) * 8 + xcd;
+    } else {
+      qg = b % p.qgroups;
+      split = b / p.qgroups;
+    }
+  }
+  // query slot of block qb is slot0 + 32 qb; Qp is a multiple of QPG so every slot exists
+  const int slot0 = qg * QPG + w * QPW2 + r32;
+
+  half8 qf[KSTEPS][2];
+#pragma unroll
+  for (int kk = 0; kk < KSTEPS; ++kk)
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb)
+      qf[kk][qb] = *(const half8*)(p.q16 + (size_t)(slot0 + 32 * qb) * DP + kk * 16 + h * 8);
+  // retire the loads here (see v1): a visible use before the loop
+#pragma unroll
+  for (int kk = 0; kk < KSTEPS; ++kk) asm volatile("" ::"a"(qf[kk][0]), "a"(qf[kk][1]));
+
+  float ls[2][KL];
+  int li[2][KL];
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+    for (int j = 0; j < KL; ++j) {
+      ls[qb][j] = -INFINITY;
+      li[qb][j] = -1;
+    }
+  float theta_f[2] = {-INFINITY, -INFINITY};
+  uint32_t theta_next[2] = {0u, 0u};
+  float published[2] = {-INFINITY, -INFINITY};
+  uint32_t* const theta_q = p.theta + slot0;
+
+  // A-fragment chunk (2j + h) of row r32 sits at chunk (2j + h) ^ (r32 & 15): byte offset
+  // offA0 ^ (j << 5), with offA0 = r32 * ROW_BYTES + 16 * (h ^ (r32 & 15))
+  const int offA0_init = r32 * ROW_BYTES + 16 * (h ^ (r32 & 15));
+
+  // acc[buffer][row block][query block]; buffer 1 starts at -inf so the first tile's
+  // (empty) predecessor epilogue is a no-op without a branch.
+  f32x16 acc[2][2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[1][i][j][r] = -INFINITY;
+      acc[0][i][j] = f32x16{};
+    }
+
+  int my_tiles = (split < p.ntiles) ? (p.ntiles - 1 - split) / p.splits + 1 : 0;
+  int tstep = p.splits;
+  if constexpr (MODE == 1) {
+    my_tiles = min(my_tiles, p.sample_tiles);
+    tstep = p.splits * p.sample_stride;
+  }
+  float smax[2] = {-INFINITY, -INFINITY};  // MODE 1: running max per query block
+
+  // `lane_t` is `lane` made opaque once per tile, so the per-piece source offsets and the
+  // A-fragment offsets are recomputed where they are used instead of being hoisted out of
+  // the tile loop into ~40 loop-carried registers
+  auto stage_piece = [&](int buf, int tile, int i, int lane_t) {
+    const char* gt = (const char*)p.x16 + (size_t)tile * TILE_BYTES;
+    const unsigned piece = w * GLDS_PER_WAVE + i;
+    const unsigned P = piece * 64 + (unsigned)lane_t;
+    const unsigned row = P / CPR;
+    const unsigned pos = P - row * CPR;
+    const unsigned c = pos ^ (row & 15);
+    glds_x4(gt + row * ROW_BYTES + c * 16, lds_base + buf * TILE_BYTES + piece * 1024);
+  };
+  auto stage_labels = [&](int buf, int tile) {
+    if (w == 0) glds_x1(p.labels + (size_t)tile * TILE_ROWS + lane, lds_base + LBL_OFF + buf * TILE_ROWS * 4);
+  };
+
+  // ---- epilogue of the previous tile: 8 group tests --------------------------------------
+  int prow = 0;  // first row of the filtered tile + 4h (its invalid rows are already -inf)
+
+  auto epi_group = [&](auto g_c, auto y_c) {
+    constexpr int G = decltype(g_c)::value;
+    constexpr int Y = decltype(y_c)::value;
+    constexpr int qb = G >> 2, rb = (G >> 1) & 1, r0 = 8 * (G & 1);
+    f32x16& av = acc[Y][rb][qb];
+    if constexpr (NO_EPI) {
+      asm volatile("" ::"v"(av));
+    } else {
+      float gm = fmaxf(fmaxf(fmaxf(av[r0], av[r0 + 1]), fmaxf(av[r0 + 2], av[r0 + 3])),
+                       fmaxf(fmaxf(av[r0 + 4], av[r0 + 5]), fmaxf(av[r0 + 6], av[r0 + 7])));
+      if constexpr (MODE == 1) {
+        smax[qb] = fmaxf(smax[qb], gm);
+        asm volatile("" : "+v"(smax[qb]));  // keep the slice in its gap
+      } else {
+        const bool hit = __any(gm > fmaxf(ls[qb][KL - 1], theta_f[qb]));
+        if (ABL != 2 && hit) {
+#pragma unroll
+          for (int r = r0; r < r0 + 8; ++r) {
+            const float sv = av[r];
+            if (sv > fmaxf(ls[qb][KL - 1], theta_f[qb]))
+              list_insert<KL>(ls[qb], li[qb], sv, prow + rb * 32 + 8 * (r >> 2) + (r & 3));
+          }
+          if (li[qb][KL - 1] >= 0 && ls[qb][KL - 1] > published[qb]) {
+            published[qb] = ls[qb][KL - 1];
+            __hip_atomic_fetch_max(theta_q + 32 * qb, mrag_f2ord(published[qb]), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+          }
+        }
+      }
+    }
+  };
+
+  // ---- one tile: MFMAs into acc[X] + the epilogue of acc[Y] in their shadow -----------
+  auto tile_body = [&](auto x_c, int it) {
+    constexpr int X = decltype(x_c)::value;
+    constexpr int Y = 1 - X;
+    const int tile = split + it * tstep;
+    const bool has_next = it + 1 < my_tiles;
+    if constexpr (MODE == 0) {
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb)
+        theta_next[qb] = __hip_atomic_load(theta_q + 32 * qb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    const int lab = ((const int*)(smem + LBL_OFF + X * TILE_ROWS * 4))[lane];
+    const bool lab_ok = (p.label_filter == MRAG_LABEL_ANY) ? (lab >= 0) : (lab == p.label_filter);
+    const uint64_t tile_mask = __ballot(lab_ok);
+    const char* tb = smem + X * TILE_BYTES;
+    int lane_t = lane, offA0 = offA0_init;
+    asm volatile("" : "+v"(lane_t), "+v"(offA0));
+    half8 a[3][2];
+    auto read_a = [&](int slot, int kk) {
+      const int o = (offA0 ^ ((kk & 7) << 5)) + (kk >> 3) * 256;
+      a[slot][0] = *(const half8*)(tb + o);
+      a[slot][1] = *(const half8*)(tb + o + 32 * ROW_BYTES);
+    };
+    read_a(0, 0);
+    if (KSTEPS > 1) read_a(1, 1);
+    if (has_next) stage_labels(Y, tile + tstep);
+    static_for<KSTEPS>([&](auto kk_c) {
+      constexpr int kk = decltype(kk_c)::value;
+      static_for<4>([&](auto j_c) {
+        constexpr int j = decltype(j_c)::value;
+        constexpr int rb = j >> 1, qb = j & 1;
+        if constexpr (kk == 0)
+          mfma_ab0(acc[X][rb][qb], a[kk % 3][rb], qf[kk][qb]);
+        else
+          mfma_ab(acc[X][rb][qb], a[kk % 3][rb], qf[kk][qb]);
+        // one job per MFMA gap (see the header)
+        constexpr int GLDS_EVERY = KSTEPS / GLDS_PER_WAVE;
+        constexpr int GROUP_EVERY = KSTEPS / NGROUPS;
+        if constexpr (j == 0) {
+          if constexpr (kk + 2 < KSTEPS) read_a((kk + 2) % 3, kk + 2);
+        } else if constexpr (j == 1) {
+          if constexpr (kk % GLDS_EVERY == 0 && !NO_GLDS) {
+            if (has_next) stage_piece(Y, tile + tstep, kk / GLDS_EVERY, lane_t);
+          }
+        } else if constexpr (j == 3) {
+          if constexpr (kk % GROUP_EVERY == 0)
+            epi_group(std::integral_constant<int, kk / GROUP_EVERY>{}, std::integral_constant<int, Y>{});
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      });
+    });
+    mfma_guard(acc[X]);
+    // rows failing the label filter drop out here (rare for unfiltered searches; kept
+    // out of the slots so its bit tests do not hold registers across the MFMA loop)
+    if (tile_mask != ~0ull) {
+      const uint64_t lm = tile_mask >> (4 * h);
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) {
+          const bool ok = row_ok(lm, rb, reg);
+          acc[X][rb][0][reg] = ok ? acc[X][rb][0][reg] : -INFINITY;
+          acc[X][rb][1][reg] = ok ? acc[X][rb][1][reg] : -INFINITY;
+        }
+    }
+    // the filtered tile is now this one
+    prow = tile * TILE_ROWS + 4 * h;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // fold in the threshold loaded at the top of this tile, here where the load has
+    // retired (used from the next tile on; pinned so hipcc's wait for it cannot land
+    // mid-tile, where it would also drain the LDS-DMA prefetch)
+    if constexpr (MODE == 0) {
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb)
+        if (theta_next[qb] != 0) theta_f[qb] = fmaxf(theta_f[qb], mrag_ord2f(theta_next[qb]));
+      asm volatile("" : "+v"(theta_f[0]), "+v"(theta_f[1]));
+    }
+    __syncthreads();
+  };
+
+  if (my_tiles > 0) {
+#pragma unroll
+    for (int i = 0; i < GLDS_PER_WAVE; ++i) stage_piece(0, split, i, lane);
+    stage_labels(0, split);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int it = 0; it < my_tiles; it += 2) {
+      tile_body(std::integral_constant<int, 0>{}, it);
+      if (it + 1 < my_tiles) tile_body(std::integral_constant<int, 1>{}, it + 1);
+    }
+    // epilogue of the last tile
+    if (my_tiles & 1) {
+      static_for<NGROUPS>([&](auto g_c) { epi_group(g_c, std::integral_constant<int, 0>{}); });
+    } else {
+      static_for<NGROUPS>([&](auto g_c) { epi_group(g_c, std::integral_constant<int, 1>{}); });
+    }
+  }
+
+  if constexpr (MODE == 1) {
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) p.part_s[((size_t)split * p.Qp + slot0 + 32 * qb) * 2 + h] = smax[qb];
+    return;
+  }
+  // fold the partner half-wave's lists (same queries, other rows) into lanes 0..31
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    float ps[KL];
+    int pi[KL];
+#pragma unroll
+    for (int j = 0; j < KL; ++j) {
+      ps[j] = __shfl_xor(ls[qb][j], 32);
+      pi[j] = __shfl_xor(li[qb][j], 32);
+    }
+    if (h == 0) {
+#pragma unroll
+      for (int j = 0; j < KL; ++j)
+        if (ps[j] > ls[qb][KL - 1]) list_insert<KL>(ls[qb], li[qb], ps[j], pi[j]);
+      const int slot = slot0 + 32 * qb;
+      float* os = p.part_s + ((size_t)split * p.Qp + slot) * KL;
+      int32_t* oi = p.part_i + ((size_t)split * p.Qp + slot) * KL;
+#pragma unroll
+      for (int j = 0; j < KL; ++j) {
+        os[j] = ls[qb][j];
+        oi[j] = li[qb][j];
+      }
+    }
+  }
+}
+
+// Seed of the shared threshold from the sample pre-pass: per query, the k-th largest of the
+// 2*splits sample maxima (maxima of disjoint row sets, so k distinct rows score at least
+// that), lowered by a margin of 2.5 EPS so that a seed equal to the k-th best approximate
+// score cannot cost the certificate (K8 includes the final threshold in T). One wave per
+// query; k rounds of wave arg-max extraction.
+constexpr float THETA_SEED_MARGIN = (float)(2.5 * EPS_F16);
+__global__ __launch_bounds__(64) void theta_init_kernel(const float* __restrict__ smax, int nvals, int Qp, int k,
+                                                        uint32_t* __restrict__ theta) {
+  constexpr int PER_LANE = 8;  // nvals = 2 * splits <= 512
+  const int q = blockIdx.x, lane = threadIdx.x;
+  float v[PER_LANE];
+#pragma unroll
+  for (int t = 0; t < PER_LANE; ++t) {
+    const int i = lane + 64 * t;
+    // value i = (split i>>1, half i&1)
+    v[t] = i < nvals ? smax[((size_t)(i >> 1) * Qp + q) * 2 + (i & 1)] : -INFINITY;
+  }
+  float kth = -INFINITY;
+  for (int r = 0; r < k; ++r) {
+    float best = -INFINITY;
+    int bt = 0;
+#pragma unroll
+    for (int t = 0; t < PER_LANE; ++t)
+      if (v[t] > best) {
+        best = v[t];
+        bt = t;
+      }
+    float wbest = best;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) wbest = fmaxf(wbest, __shfl_xor(wbest, off));
+    if (wbest == -INFINITY) {
+      kth = -INFINITY;
+      break;
+    }
+    // remove exactly one occurrence: the lowest lane holding the maximum
+    const uint64_t holders = __ballot(best == wbest);
+    if (lane == (int)__builtin_ctzll(holders)) {
+#pragma unroll
+      for (int t = 0; t < PER_LANE; ++t)
+        if (t == bt) v[t] = -INFINITY;
+    }
+    kth = wbest;
+  }
+  if (lane == 0) theta[q] = (kth == -INFINITY) ? 0u : mrag_f2ord(kth - THETA_SEED_MARGIN);
+}
+
+// ---------------------------------------------------------------------------
 // Exact rescoring helper: one wave computes q.x in f64 (fixed lane-strided order
 // + fixed butterfly => deterministic) and returns the cosine on lane 0..63.
 __device__ __forceinline__ double exact_cosine(const float* qs, double qn, const float* __restrict__ x32,
@@ -382,6 +756,7 @@ struct MergeParams {
   float* thresh;
   int32_t* fail_list;
   int32_t* fail_cnt;
+  const uint32_t* theta;  // final shared threshold (rows at or below it were never listed)
 };
 
 __device__ __forceinline__ float f32_round_down(double x) {
@@ -459,7 +834,12 @@ __global__ __launch_bounds__(MERGE_THREADS) void knn_merge_kernel(MergeParams p)
 
   const int M = min(p.M, valid);
   const float a_next = (valid > M) ? mrag_ord2f(~(uint32_t)(keys[M] >> 32)) : -INFINITY;
-  const double T = (double)fmaxf(tau, a_next);
+  // every row outside the candidate set scores <= T by approximation: rejected by a full
+  // list (<= tau), by the shared threshold (<= theta; a seeded theta need not be any
+  // list's KL-th, so it is bounded separately), or beyond the M-th candidate (<= a_next)
+  float th = -INFINITY;
+  if (p.theta && p.theta[q] != 0u) th = mrag_ord2f(p.theta[q]);
+  const double T = (double)fmaxf(fmaxf(tau, a_next), th);
   const double qn = p.qn[q];
 
   for (int m = wave; m < p.Mp; m += MERGE_THREADS / 64) {
@@ -769,6 +1149,16 @@ int kl_for(int k, int DP) {
   return 32;
 }
 
+scan_fn get_scan2(int DP, bool sample = false) {
+  switch (DP) {
+    case 128: return sample ? knn_scan2_kernel<128, 0, 1> : knn_scan2_kernel<128>;
+    case 256: return sample ? knn_scan2_kernel<256, 0, 1> : knn_scan2_kernel<256>;
+    case 384: return sample ? knn_scan2_kernel<384, 0, 1> : knn_scan2_kernel<384>;
+    case 512: return sample ? knn_scan2_kernel<512, 0, 1> : knn_scan2_kernel<512>;
+    default: return nullptr;
+  }
+}
+
 scan_fn get_scan(int DP, int KL, bool collect) {
   switch (DP) {
     case 128: return pick_scan<128>(KL, collect);
@@ -798,6 +1188,8 @@ struct mrag_knn_index {
   DevBuf qin, q32, qn, q16, part_s, part_i, thresh, fail_list, counters, cand_cnt, cand, scratch;
   DevBuf out_s, out_s64, out_r, stage_rows, stage_labels, rowlist, theta;
   int ablate = 0;  // diagnostic knob, env MRAG_SCAN_ABLATE (timing experiments only)
+  bool scan_v1 = false;  // env MRAG_SCAN_V1=1: force the v1 top-k scan (A/B timing)
+  bool no_sample = false;  // env MRAG_SCAN_NO_SAMPLE=1: skip the threshold pre-pass (A/B timing)
   int32_t* host_counters = nullptr;  // pinned [2]: fail_cnt, overflow
   int ccap = 4096;
   int64_t last_uncertified = 0, last_retries = 0;
@@ -862,6 +1254,8 @@ int mrag_knn_create(int32_t dim, int32_t device, mrag_knn_index** out) {
   ix->D = dim;
   ix->DP = (dim + 127) / 128 * 128;
   if (const char* ab = getenv("MRAG_SCAN_ABLATE")) ix->ablate = atoi(ab);
+  if (const char* v1 = getenv("MRAG_SCAN_V1")) ix->scan_v1 = atoi(v1) != 0;
+  if (const char* ns = getenv("MRAG_SCAN_NO_SAMPLE")) ix->no_sample = atoi(ns) != 0;
   hipError_t e = hipStreamCreateWithFlags(&ix->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipHostMalloc((void**)&ix->host_counters, 16, hipHostMallocDefault);
   if (e != hipSuccess) {
@@ -1016,10 +1410,15 @@ int mrag_knn_search(mrag_knn_index* ix, const float* queries, int64_t nq, int32_
                        orr, nout);
     MRAG_CHECK_LAUNCH();
   } else {
-    const int64_t Qp = (nq + QPW - 1) / QPW * QPW;
+    // v2 (64 queries/wave, KL = 8) unless k is deep enough to want longer per-lane lists
+    const bool use_v2 = k <= 32 && !ix->scan_v1 && (ix->ablate == 0 || ix->ablate >= 10);
+    // query slots: v2 reads every slot of its query group (no lane guard), so pad to a
+    // whole group; padding rows are zero (prep) and never reach the output
+    const int64_t qpad = use_v2 ? QPG : QPW;
+    const int64_t Qp = (nq + qpad - 1) / qpad * qpad;
     const int qgroups = (int)((Qp + QPG - 1) / QPG);
     const int ntiles = (int)((ix->n + TILE_ROWS - 1) / TILE_ROWS);
-    const int KL = kl_for(k, DP);
+    const int KL = use_v2 ? 8 : kl_for(k, DP);
     int S = std::max(1, 256 / qgroups);
     S = std::min(S, ntiles);
     S = std::min(S, MAX_MERGE_ENTRIES / KL);
@@ -1070,13 +1469,34 @@ int mrag_knn_search(mrag_knn_index* ix, const float* queries, int64_t nq, int32_
     sp.thresh = (const float*)ix->thresh.p;
     sp.cand_cnt = (int32_t*)ix->cand_cnt.p;
 
-    scan_fn scan = get_scan(DP, KL, false);
+    scan_fn scan = use_v2 ? get_scan2(DP) : get_scan(DP, KL, false);
+    if (DP == 512 && ix->ablate > 10) {  // timing only
+      switch (ix->ablate) {
+        case 11: scan = knn_scan2_kernel<512, 1>; break;
+        case 12: scan = knn_scan2_kernel<512, 2>; break;
+            case 14: scan = knn_scan2_kernel<512, 4>; break;
+        default: break;
+      }
+    }
     if (ix->ablate == 1 && DP == 512) scan = knn_scan_kernel<512, 8, false, true>;  // timing only
     scan_fn collect = get_scan(DP, 8, true);
     if (!scan || !collect) return mrag::fail(MRAG_ERR_UNSUPPORTED, "no scan kernel for DP=%d", DP);
     const dim3 sgrid((unsigned)(qgroups * S));
+    // Sample pre-pass (v2 only, when every split has >= 64 tiles): seeds the shared
+    // threshold near the k-th best so the main scan's list insertions stay rare.
+    const int sample_stride = 16;
+    const int min_tiles = ntiles / S;
+    if (use_v2 && !ix->no_sample && min_tiles >= 4 * sample_stride) {
+      sp.sample_stride = sample_stride;
+      sp.sample_tiles = min_tiles / sample_stride;
+      hipLaunchKernelGGL(get_scan2(DP, true), sgrid, dim3(SCAN2_THREADS), 0, s, sp);
+      MRAG_CHECK_LAUNCH();
+      hipLaunchKernelGGL(theta_init_kernel, dim3((unsigned)nq), dim3(64), 0, s, (const float*)sp.part_s, 2 * S,
+                         (int)Qp, k, sp.theta);
+      MRAG_CHECK_LAUNCH();
+    }
     if (ix->profile) MRAG_HIP(hipEventRecord(ix->ev0, s));
-    hipLaunchKernelGGL(scan, sgrid, dim3(SCAN_THREADS), 0, s, sp);
+    hipLaunchKernelGGL(scan, sgrid, dim3(use_v2 ? SCAN2_THREADS : SCAN_THREADS), 0, s, sp);
     MRAG_CHECK_LAUNCH();
     if (ix->profile) MRAG_HIP(hipEventRecord(ix->ev1, s));
 
@@ -1104,6 +1524,7 @@ int mrag_knn_search(mrag_knn_index* ix, const float* queries, int64_t nq, int32_
     mp.thresh = (float*)ix->thresh.p;
     mp.fail_list = (int32_t*)ix->fail_list.p;
     mp.fail_cnt = (int32_t*)ix->counters.p;
+    mp.theta = (const uint32_t*)ix->theta.p;
     const size_t msh = (size_t)R * 8 + (size_t)Mp * 12 + (size_t)DP * 4 + 64;
     hipLaunchKernelGGL(knn_merge_kernel, dim3((unsigned)nq), dim3(MERGE_THREADS), msh, s, mp);
     MRAG_CHECK_LAUNCH();

@@ -187,3 +187,25 @@ def test_full_size_1m_x_512(cuda):
     _check(s.cpu().numpy()[sel], r[sel], os_, or_)
     unc, _ = ix.last_stats()
     assert unc == 0
+
+
+@pytest.mark.parametrize("label_filter", [-1, 2])
+def test_seeded_threshold_prepass(cuda, label_filter):
+    """Large enough that the sample pre-pass seeds the shared threshold (every split
+    holds >= 64 tiles: 270k rows, 1000 queries -> 64 splits x 65 tiles). Clustered
+    near-duplicates and exact duplicates make the seed land close to the true k-th score
+    (ties at the seed margin), with and without a label prefilter; results must still be
+    exact and in (score desc, row asc) order."""
+    from app.vector_store import FlatIndex
+
+    x = clustered_corpus(270_000, 128, 11, n_clusters=64, spread=0.05, dup_frac=0.05)
+    lab = labels_for(len(x), 4, 12)
+    rng = np.random.default_rng(13)
+    q = np.concatenate([x[rng.integers(0, len(x), 500)] + 0.01 * rng.standard_normal((500, 128)).astype(np.float32),
+                        rng.standard_normal((500, 128)).astype(np.float32)])
+    ix = FlatIndex(128)
+    ix.add(x, lab)
+    for k in (1, 10, 32):
+        s, r = ix.search(q, k, label=label_filter)
+        os_, or_ = flat_cosine_topk(x, lab, q, k, label_filter=label_filter)
+        _check(s, r, os_, or_)
