@@ -34,6 +34,32 @@ __device__ __forceinline__ void glds_x4(const void* gsrc, uint32_t lds_addr) {
 // Operands staged to LDS by LDS-DMA, 128-byte rows with chunk c stored at position
 // c ^ ((row >> 1) & 7) (source-address swizzle) so every ds_read_b128 fragment read is
 // bank-conflict free; 2 stages, one barrier per 64-deep k-step.
+template <int EPI>
+__device__ __forceinline__ void gemm_store(const GemmArgs& g, int m, int n, float v) {
+  const size_t o = (size_t)m * g.ldc + n;
+  if constexpr (EPI == EPI_F16) {
+    ((_Float16*)g.C)[o] = (_Float16)v;
+  } else if constexpr (EPI == EPI_F16_QUICK_GELU) {
+    // x * sigmoid(1.702 x) with hardware exp2 / rcp (~1 ulp each; the result is rounded
+    // to fp16) instead of a full-precision divide
+    v = v * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.702f * 1.44269504088896341f * v));
+    ((_Float16*)g.C)[o] = (_Float16)v;
+  } else if constexpr (EPI == EPI_F16_GELU_ERF) {
+    v = 0.5f * v * (1.0f + erff(v * 0.70710678118654752f));
+    ((_Float16*)g.C)[o] = (_Float16)v;
+  } else if constexpr (EPI == EPI_F32_RESIDUAL) {
+    ((float*)g.C)[o] += v;
+  } else {
+    ((float*)g.C)[o] = v;
+  }
+}
+
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  // blocks bid, bid+8, ... share an XCD; give each XCD a contiguous range of tile ids
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+}
+
 constexpr int GM = 128, GN = 128, GK = 64;
 constexpr int GTHREADS = 256;
 constexpr int STAGE_BYTES = (GM + GN) * GK * 2;  // 32 KiB
@@ -120,22 +146,137 @@ __global__ __launch_bounds__(GTHREADS) void gemm_nt_kernel(GemmArgs g) {
 #pragma unroll
       for (int reg = 0; reg < 16; ++reg) {
         const int m = m0 + wr * 64 + i * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
-        if (m >= g.M) continue;
-        float v = acc[i][j][reg] + bn;
-        const size_t o = (size_t)m * g.ldc + n;
-        if constexpr (EPI == EPI_F16) {
-          ((_Float16*)g.C)[o] = (_Float16)v;
-        } else if constexpr (EPI == EPI_F16_QUICK_GELU) {
-          v = v / (1.0f + __expf(-1.702f * v));
-          ((_Float16*)g.C)[o] = (_Float16)v;
-        } else if constexpr (EPI == EPI_F16_GELU_ERF) {
-          v = 0.5f * v * (1.0f + erff(v * 0.70710678118654752f));
-          ((_Float16*)g.C)[o] = (_Float16)v;
-        } else if constexpr (EPI == EPI_F32_RESIDUAL) {
-          ((float*)g.C)[o] += v;
-        } else {
-          ((float*)g.C)[o] = v;
+        // one epilogue for every GEMM kernel: a row's result must not depend on which
+        // kernel the batch size selected
+        if (m < g.M) gemm_store<EPI>(g, m, n, acc[i][j][reg] + bn);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// K3b: the same GEMM for the big-M encoder batches (M >= 1024 rows: ViT at batch 256 is
+// M = 12,800), 256 x BN block tile, 8 waves as 2 (M) x 4 (N) of 128 x BN/4, BK = 64.
+// One workgroup per CU (128 KiB LDS at BN = 256): each A fragment read from LDS feeds
+// BN/128 MFMAs and each B fragment four, half the LDS bytes per MFMA of K3.
+// Pipeline per 64-deep k-step: the next k-step's tile is staged by LDS-DMA in pieces
+// spread over the four 16-deep sub-steps (one job per MFMA cluster), the fragments of
+// sub-step kk+1 are read while the MFMAs of kk run (two register sets), and one
+// vmcnt(0) + barrier closes the k-step. Block ids are remapped so that the blocks of one
+// A panel (same tm) run on the same XCD (bijective for any grid size).
+constexpr int GB_BM = 256, GB_THREADS = 512;
+
+template <int BN, int EPI, bool EARLY = true>
+__global__ __launch_bounds__(GB_THREADS) void gemm_big_kernel(GemmArgs g) {
+  constexpr int WN = BN / 4;                   // wave tile 128 x WN
+  constexpr int TM = 4, TN = WN / 32;          // 32x32 blocks per wave
+  constexpr int A_BYTES = GB_BM * GK * 2;      // 32 KiB
+  constexpr int STAGE = (GB_BM + BN) * GK * 2;
+  constexpr int PIECES = (GB_BM + BN) / 8;     // 1 KiB = 8 rows x 128 B
+  constexpr int PPW = PIECES / 8;              // per wave per k-step
+  static_assert(PIECES % 8 == 0 && PPW <= 8, "pieces per wave");
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = w >> 2, wc = w & 3;
+  const int h = lane >> 5, r32 = lane & 31;
+  const uint32_t lds_base = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)((AS3 char*)smem));
+
+  const int tiles_n = g.N / BN;
+  const int nwg = gridDim.x;
+  const int t = xcd_remap(blockIdx.x, nwg);
+  const int tm = t / tiles_n, tn = t - (t / tiles_n) * tiles_n;
+  const int m0 = tm * GB_BM, n0 = tn * BN;
+  const int ksteps = g.K / GK;
+
+  // piece P of a stage: rows 8(P mod ...) .. +8 of A (P < 32) or of W; lane -> row rr, chunk pos
+  auto stage_piece = [&](int buf, int k0, int i) {
+    const int P = w * PPW + i;
+    const int rr = lane >> 3, pos = lane & 7;
+    const _Float16* src;
+    int row;
+    if (P < GB_BM / 8) {
+      row = 8 * P + rr;
+      const int c = pos ^ ((row >> 1) & 7);
+      src = g.A + (size_t)min(m0 + row, g.M - 1) * g.lda + k0 + c * 8;
+    } else {
+      row = 8 * (P - GB_BM / 8) + rr;
+      const int c = pos ^ ((row >> 1) & 7);
+      src = g.W + (size_t)(n0 + row) * g.ldw + k0 + c * 8;
+    }
+    glds_x4(src, lds_base + buf * STAGE + P * 1024);
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x16{};
+
+  const int sw = (r32 >> 1) & 7;
+  // fragment offsets (bytes within a stage): A row wr*128 + 32i + r32, B row wc*WN + 32j + r32
+  const int offA = (wr * 128 + r32) * 128;
+  const int offB = A_BYTES + (wc * WN + r32) * 128;
+  half8 fa[2][TM], fb[2][TN];
+  auto read_frags = [&](int set, int buf, int kk) {
+    const char* st = (const char*)smem + buf * STAGE;
+    const int coff = ((2 * kk + h) ^ sw) * 16;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) fa[set][i] = *(const half8*)(st + offA + i * 32 * 128 + coff);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) fb[set][j] = *(const half8*)(st + offB + j * 32 * 128 + coff);
+  };
+
+#pragma unroll
+  for (int i = 0; i < PPW; ++i) stage_piece(0, 0, i);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int ks = 0; ks < ksteps; ++ks) {
+    const int cur = ks & 1;
+    const bool more = ks + 1 < ksteps;
+    read_frags(0, cur, 0);
+#pragma unroll
+    for (int kk = 0; kk < GK / 16; ++kk) {
+      const int set = kk & 1;
+      if (kk + 1 < GK / 16) read_frags(set ^ 1, cur, kk + 1);
+      // next k-step's pieces: all at the first sub-step (EARLY: a full k-step of latency
+      // cover before the closing vmcnt(0)), or spread over the four sub-steps
+      if constexpr (EARLY) {
+        if (kk == 0) {
+#pragma unroll
+          for (int i = 0; i < PPW; ++i)
+            if (more) stage_piece(cur ^ 1, (ks + 1) * GK, i);
         }
+      } else {
+#pragma unroll
+        for (int i = kk * PPW / 4; i < (kk + 1) * PPW / 4; ++i)
+          if (more) stage_piece(cur ^ 1, (ks + 1) * GK, i);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[set][i], fb[set][j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  // epilogue: lane owns column n of each 32x32 block and rows (reg&3)+8(reg>>2)+4h
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int n = n0 + wc * WN + j * 32 + r32;
+    const float bn = g.bias ? g.bias[n] : 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) {
+        const int m = m0 + wr * 128 + i * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+        if (m < g.M) gemm_store<EPI>(g, m, n, acc[i][j][reg] + bn);
       }
     }
   }
@@ -472,11 +613,42 @@ __global__ void mean_pool_kernel(const float* __restrict__ X, const int32_t* __r
 
 // ---------------------------------------------------------------------------
 // launchers
+// env MRAG_GEMM_BIG (A/B timing): default -1 = K3b (BN 256 when N % 256 == 0, else 128) from
+// M >= 1024; 0 = K3 only; 256 / 128 = K3b at that tile width; 2 = K3b with the LDS-DMA spread
+int gemm_big_mode() {
+  static const int v = [] {
+    const char* e = getenv("MRAG_GEMM_BIG");
+    return e ? atoi(e) : -1;
+  }();
+  return v;
+}
+
+template <int BN, bool EARLY>
+int launch_gemm_big(const GemmArgs& g, int epi, hipStream_t s) {
+  const dim3 grid((unsigned)(((g.M + GB_BM - 1) / GB_BM) * (g.N / BN)));
+  switch (epi) {
+    case EPI_F16: hipLaunchKernelGGL((gemm_big_kernel<BN, EPI_F16, EARLY>), grid, dim3(GB_THREADS), 0, s, g); break;
+    case EPI_F16_QUICK_GELU: hipLaunchKernelGGL((gemm_big_kernel<BN, EPI_F16_QUICK_GELU, EARLY>), grid, dim3(GB_THREADS), 0, s, g); break;
+    case EPI_F16_GELU_ERF: hipLaunchKernelGGL((gemm_big_kernel<BN, EPI_F16_GELU_ERF, EARLY>), grid, dim3(GB_THREADS), 0, s, g); break;
+    case EPI_F32_RESIDUAL: hipLaunchKernelGGL((gemm_big_kernel<BN, EPI_F32_RESIDUAL, EARLY>), grid, dim3(GB_THREADS), 0, s, g); break;
+    case EPI_F32: hipLaunchKernelGGL((gemm_big_kernel<BN, EPI_F32, EARLY>), grid, dim3(GB_THREADS), 0, s, g); break;
+    default: return mrag::fail(MRAG_ERR_ARG, "gemm: bad epilogue %d", epi);
+  }
+  MRAG_CHECK_LAUNCH();
+  return MRAG_OK;
+}
+
 int launch_gemm(const GemmArgs& g, int epi, hipStream_t s) {
   if (g.M <= 0) return MRAG_OK;
   MRAG_REQUIRE(g.N % GN == 0 && g.K % GK == 0, "gemm: N=%d must be a multiple of %d and K=%d of %d", g.N, GN, g.K,
                GK);
   MRAG_REQUIRE(g.lda % 8 == 0 && g.ldw % 8 == 0, "gemm: lda/ldw must be multiples of 8");
+  const int big = gemm_big_mode();
+  if (g.M >= 1024 && big != 0) {
+    if (big == 2) return g.N % 256 == 0 ? launch_gemm_big<256, false>(g, epi, s) : launch_gemm_big<128, false>(g, epi, s);
+    if ((big == -1 || big == 256) && g.N % 256 == 0) return launch_gemm_big<256, true>(g, epi, s);
+    if (big != 256) return launch_gemm_big<128, true>(g, epi, s);  // N % 128 == 0 (checked above)
+  }
   const dim3 grid((unsigned)(((g.M + GM - 1) / GM) * (g.N / GN)));
   switch (epi) {
     case EPI_F16: hipLaunchKernelGGL(gemm_nt_kernel<EPI_F16>, grid, dim3(GTHREADS), 0, s, g); break;

@@ -104,6 +104,15 @@ __device__ __forceinline__ void glds_x4(const void* gsrc, uint32_t lds_addr) {
       : "v"(gsrc), "s"(lds_addr)
       : "memory");
 }
+// SADDR form: wave-uniform 64-bit base in SGPRs + per-lane 32-bit offset (no 64-bit VALU)
+__device__ __forceinline__ void glds_x4_saddr(uint32_t voff, const void* sbase, uint32_t lds_addr) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(sbase), "s"(lds_addr)
+      : "memory");
+}
 __device__ __forceinline__ void glds_x1(const void* gsrc, uint32_t lds_addr) {
   unsigned keep;
   asm volatile(
@@ -511,6 +520,11 @@ __global__ __launch_bounds__(SCAN2_THREADS) void knn_scan2_kernel(ScanParams p) 
     const unsigned c = pos ^ (row & 15);
     glds_x4(gt + row * ROW_BYTES + c * 16, lds_base + buf * TILE_BYTES + piece * 1024);
   };
+  // DP = 512: piece i of wave w is corpus row w * 16 + i of the tile, so its source is one
+  // per-tile SGPR base + a lane offset 16 * (lane ^ i) + 1024 i (one VALU op per piece)
+  auto stage_row = [&](const char* gw, uint32_t ldsw, int i, uint32_t lane16) {
+    glds_x4_saddr((lane16 ^ (uint32_t)(i << 4)) + (uint32_t)(i * 1024), gw, ldsw + i * 1024);
+  };
   auto stage_labels = [&](int buf, int tile) {
     if (w == 0) glds_x1(p.labels + (size_t)tile * TILE_ROWS + lane, lds_base + LBL_OFF + buf * TILE_ROWS * 4);
   };
@@ -556,6 +570,12 @@ __global__ __launch_bounds__(SCAN2_THREADS) void knn_scan2_kernel(ScanParams p) 
     constexpr int Y = 1 - X;
     const int tile = split + it * tstep;
     const bool has_next = it + 1 < my_tiles;
+    // source of the next tile's pieces (the last tile restages itself into the idle buffer
+    // instead of branching around every piece)
+    const int ntile = has_next ? tile + tstep : tile;
+    const char* gw = (const char*)p.x16 + (size_t)ntile * TILE_BYTES + (size_t)w * GLDS_PER_WAVE * ROW_BYTES;
+    uint32_t ldsw = lds_base + Y * TILE_BYTES + w * GLDS_PER_WAVE * 1024;
+    asm volatile("" : "+s"(gw), "+s"(ldsw));
     if constexpr (MODE == 0) {
 #pragma unroll
       for (int qb = 0; qb < 2; ++qb)
@@ -566,7 +586,8 @@ __global__ __launch_bounds__(SCAN2_THREADS) void knn_scan2_kernel(ScanParams p) 
     const uint64_t tile_mask = __ballot(lab_ok);
     const char* tb = smem + X * TILE_BYTES;
     int lane_t = lane, offA0 = offA0_init;
-    asm volatile("" : "+v"(lane_t), "+v"(offA0));
+    uint32_t lane16 = lane * 16;
+    asm volatile("" : "+v"(lane_t), "+v"(offA0), "+v"(lane16));
     half8 a[3][2];
     auto read_a = [&](int slot, int kk) {
       const int o = (offA0 ^ ((kk & 7) << 5)) + (kk >> 3) * 256;
@@ -575,7 +596,7 @@ __global__ __launch_bounds__(SCAN2_THREADS) void knn_scan2_kernel(ScanParams p) 
     };
     read_a(0, 0);
     if (KSTEPS > 1) read_a(1, 1);
-    if (has_next) stage_labels(Y, tile + tstep);
+    stage_labels(Y, ntile);
     static_for<KSTEPS>([&](auto kk_c) {
       constexpr int kk = decltype(kk_c)::value;
       static_for<4>([&](auto j_c) {
@@ -592,7 +613,10 @@ __global__ __launch_bounds__(SCAN2_THREADS) void knn_scan2_kernel(ScanParams p) 
           if constexpr (kk + 2 < KSTEPS) read_a((kk + 2) % 3, kk + 2);
         } else if constexpr (j == 1) {
           if constexpr (kk % GLDS_EVERY == 0 && !NO_GLDS) {
-            if (has_next) stage_piece(Y, tile + tstep, kk / GLDS_EVERY, lane_t);
+            if constexpr (CPR == 64)
+              stage_row(gw, ldsw, kk / GLDS_EVERY, lane16);
+            else
+              stage_piece(Y, ntile, kk / GLDS_EVERY, lane_t);
           }
         } else if constexpr (j == 3) {
           if constexpr (kk % GROUP_EVERY == 0)

@@ -1,0 +1,63 @@
+"""K3/K3b GEMM microbenchmark on the ViT-B/32 batch-256 shapes (+ 4096^3 reference).
+
+python scripts/gemm_bench.py [shape ...]   shapes: qkv fc1 fc2 out sq4k (default: all)
+Each shape: random fp16 operands, 5 warmup + 20 timed launches, HIP events.
+"""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "multimodal-rag-for-image-text-search_amd"), ROOT]
+
+import torch  # noqa: E402
+
+from app.encoders import gemm_nt  # noqa: E402
+
+SHAPES = {  # name: (M, N, K, epilogue)
+    "qkv": (12800, 2304, 768, 0),
+    "fc1": (12800, 3072, 768, 1),
+    "fc2": (12800, 768, 3072, 3),
+    "out": (12800, 768, 768, 3),
+    "sq4k": (4096, 4096, 4096, 0),
+}
+
+
+def run(name, reps=20):
+    M, N, K, epi = SHAPES[name]
+    g = torch.Generator(device="cuda").manual_seed(0)
+    A = (torch.rand(M, K, generator=g, device="cuda") * 2 - 1).half()
+    W = (torch.rand(N, K, generator=g, device="cuda") * 2 - 1).half()
+    bias = torch.zeros(N, device="cuda")
+    C = torch.zeros(M, N, device="cuda", dtype=torch.float16 if epi <= 2 else torch.float32)
+    for _ in range(5):
+        gemm_nt(A, W, bias, C, epi)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        gemm_nt(A, W, bias, C, epi)
+    e1.record()
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) * 1e3 / reps
+    out = {"shape": name, "M": M, "N": N, "K": K, "us": round(us, 1), "TFLOPs": round(2 * M * N * K / us / 1e6, 1)}
+    if os.environ.get("TORCH_REF") == "1":  # vendor library on the same shape (reference point only)
+        Wt = W.t()
+        for _ in range(5):
+            torch.matmul(A, Wt)
+        torch.cuda.synchronize()
+        e0.record()
+        for _ in range(reps):
+            torch.matmul(A, Wt)
+        e1.record()
+        torch.cuda.synchronize()
+        tus = e0.elapsed_time(e1) * 1e3 / reps
+        out["torch_us"] = round(tus, 1)
+        out["torch_TFLOPs"] = round(2 * M * N * K / tus / 1e6, 1)
+    return out
+
+
+if __name__ == "__main__":
+    names = sys.argv[1:] or list(SHAPES)
+    for n in names:
+        print(json.dumps(run(n)), flush=True)

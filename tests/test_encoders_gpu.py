@@ -65,6 +65,39 @@ def test_gemm_epilogues(cuda, epi):
     assert err < 1e-2, err
 
 
+@pytest.mark.parametrize("M,N,K", [(1100, 768, 768), (2048, 384, 320), (1024, 2304, 192)])
+@pytest.mark.parametrize("epi", [0, 1, 2, 3, 4])
+def test_gemm_big_tiles(cuda, M, N, K, epi):
+    """K3b (256-row tiles, used from M = 1024): ragged M (1100 = 4 x 256 + 76), both tile
+    widths (N % 256 == 0 -> 256, else 128), every epilogue; same tolerance as K3."""
+    import torch
+
+    from app.encoders import gemm_nt
+
+    g = torch.Generator(device=cuda).manual_seed(7 + epi)
+    A = (torch.randn(M, K, generator=g, device=cuda) * 0.5).half()
+    W = (torch.randn(N, K, generator=g, device=cuda) * 0.05).half()
+    bias = torch.randn(N, generator=g, device=cuda) * 0.1
+    ref = A.float() @ W.float().t() + bias
+    if epi == 1:
+        ref = ref * torch.sigmoid(1.702 * ref)
+    elif epi == 2:
+        ref = torch.nn.functional.gelu(ref)
+    if epi <= 2:
+        C = torch.full((M, N), float("nan"), dtype=torch.float16, device=cuda)
+    elif epi == 3:
+        C0 = torch.randn(M, N, generator=g, device=cuda)
+        C = C0.clone()
+        ref = ref + C0
+    else:
+        C = torch.full((M, N), float("nan"), dtype=torch.float32, device=cuda)
+    gemm_nt(A, W, bias, C, epi)
+    torch.cuda.synchronize()
+    assert not torch.isnan(C.float()).any()
+    err = (C.float() - ref).abs().max().item() / ref.abs().max().item()
+    assert err < 1e-2, err
+
+
 @pytest.fixture(scope="module")
 def vision(cuda):
     from app.encoders import CLIP_VISION_B32, GpuEncoder
