@@ -170,6 +170,16 @@ int mrag_encoder_embed_images(mrag_encoder* enc, const uint8_t* images, int32_t 
 int mrag_encoder_embed_tokens(mrag_encoder* enc, const int32_t* ids, const int32_t* mask, int32_t batch,
                               int32_t seq, float* out, int32_t normalize, int32_t ptr_kind, void* stream);
 
+/* K0: image resize (shortest edge -> size, bicubic) + centre crop, bit-exact to the
+ * reference's preprocessing (CLIPImageProcessor -> PIL.Image.resize(BICUBIC) + center_crop,
+ * app/ml/embeddings.py:84-85; host restatement app/encoders/preprocess.py:to_u8_224).
+ * pixels: device u8 RGB HWC images, image i at byte offset offsets[i] with size
+ * widths[i] x heights[i] (offsets/widths/heights are host arrays of n entries);
+ * out: device u8 [n][size][size][3] (the input of mrag_encoder_embed_images).
+ * Synchronous on `stream` (returns after the kernels finish). */
+int mrag_image_resize_crop(const uint8_t* pixels, const int64_t* offsets, const int32_t* widths,
+                           const int32_t* heights, int32_t n, int32_t size, uint8_t* out, void* stream);
+
 /* K3 building block: C[M][N] (op)= A[M][K] . W[N][K]^T + bias (device pointers;
  * A, W fp16 row-major; epilogue 0 f16 out, 1 f16 quick_gelu, 2 f16 gelu_erf,
  * 3 f32 C += , 4 f32 out). N % 128 == 0, K % 64 == 0. */

@@ -19,7 +19,7 @@ from typing import Optional, Sequence
 import numpy as np
 
 from app.encoders import CLIP_TEXT_B32, CLIP_VISION_B32, MINILM_L6, load_encoder
-from app.encoders.preprocess import load_batch
+from app.encoders.preprocess import load_batch, load_batch_device
 from app.encoders.tokenize import ClipTokenizer, WordPieceTokenizer
 
 
@@ -136,7 +136,9 @@ class ClipProcessor:
 
     def __call__(self, *, images=None, text=None, return_tensors="pt", padding=None, **kw):
         if images is not None:
-            return BatchInputs(images_u8=load_batch(list(images)))
+            if os.environ.get("MRAG_HOST_RESIZE") == "1":  # A/B: PIL resize on the host
+                return BatchInputs(images_u8=load_batch(list(images)))
+            return BatchInputs(images_u8=load_batch_device(list(images), device=_device_index()))
         if text is not None:
             ids, mask = self.tokenizer(list(text))
             return BatchInputs(input_ids=ids, attention_mask=mask)

@@ -1,6 +1,11 @@
-"""Host image preprocessing: decode -> RGB -> resize (shortest edge 224, bicubic) ->
-centre crop 224 -> u8 HWC. Everything after (rescale, mean/std normalise, layout) is
-fused into the GPU patch-embed kernel.
+"""Image preprocessing: decode -> RGB -> resize (shortest edge 224, bicubic) -> centre
+crop 224 -> u8 HWC. Everything after (rescale, mean/std normalise, layout) is fused into
+the GPU patch-embed kernel.
+
+Two implementations with identical bytes: ``load_batch_device`` (the default for the
+native encoders) decodes on host threads and runs the resize + crop on the GPU
+(``mrag_image_resize_crop``, K0 in csrc/imgprep.hip — Pillow's fixed-point resampler
+restated); ``load_batch`` does all of it with PIL on the host.
 
 Restates CLIPImageProcessor's PIL path (the processor the reference loads for
 openai/clip-vit-base-patch32, app/ml/embeddings.py:39-43, 84-85):
@@ -55,3 +60,59 @@ def load_batch(items: Sequence[Union[str, Path, Image.Image]], workers: int = 8)
         return np.empty((0, SIZE, SIZE, 3), dtype=np.uint8)
     with ThreadPoolExecutor(max_workers=max(1, min(workers, len(items)))) as ex:
         return np.stack(list(ex.map(one, items)))
+
+
+def decode_rgb(x: Union[str, Path, Image.Image]) -> np.ndarray:
+    """Decode only: u8 HxWx3 RGB (the part of preprocessing that stays on the host)."""
+    if isinstance(x, Image.Image):
+        return np.asarray(x if x.mode == "RGB" else x.convert("RGB"), dtype=np.uint8)
+    with Image.open(x) as im:
+        return np.asarray(im.convert("RGB"), dtype=np.uint8)
+
+
+def resize_crop_device(arrays: Sequence[np.ndarray], device: int = 0, size: int = SIZE):
+    """u8 HxWx3 host arrays -> u8 [n, size, size, 3] CUDA tensor, resized + centre-cropped
+    on the GPU (bit-identical to ``to_u8_224``)."""
+    import ctypes
+
+    import torch
+
+    from app import _native
+
+    n = len(arrays)
+    dev = torch.device("cuda", device)
+    out = torch.empty((n, size, size, 3), dtype=torch.uint8, device=dev)
+    if n == 0:
+        return out
+    arrays = [np.ascontiguousarray(a, dtype=np.uint8) for a in arrays]
+    for a in arrays:
+        if a.ndim != 3 or a.shape[2] != 3:
+            raise ValueError(f"expected HxWx3 u8 images, got shape {a.shape}")
+    sizes = np.array([a.size for a in arrays], dtype=np.int64)
+    offsets = np.zeros(n, dtype=np.int64)
+    offsets[1:] = np.cumsum(sizes)[:-1]
+    host = torch.empty(int(sizes.sum()), dtype=torch.uint8, pin_memory=True)
+    hv = host.numpy()
+    for a, o, sz in zip(arrays, offsets, sizes):
+        hv[o:o + sz] = a.reshape(-1)
+    pix = host.to(dev, non_blocking=True)
+    widths = np.array([a.shape[1] for a in arrays], dtype=np.int32)
+    heights = np.array([a.shape[0] for a in arrays], dtype=np.int32)
+    with torch.cuda.device(dev):
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        _native.call("mrag_image_resize_crop", pix.data_ptr(),
+                     offsets.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+                     widths.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                     heights.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), n, size, out.data_ptr(), stream)
+    return out
+
+
+def load_batch_device(items: Sequence[Union[str, Path, Image.Image]], device: int = 0, workers: int = 8):
+    """Decode on a host thread pool, resize + crop on the GPU: u8 [n, 224, 224, 3] CUDA tensor."""
+    if len(items) == 0:
+        import torch
+
+        return torch.empty((0, SIZE, SIZE, 3), dtype=torch.uint8, device=torch.device("cuda", device))
+    with ThreadPoolExecutor(max_workers=max(1, min(workers, len(items)))) as ex:
+        arrays = list(ex.map(decode_rgb, items))
+    return resize_crop_device(arrays, device=device)
