@@ -127,6 +127,10 @@ int mrag_topk_merge(const double* scores64, const int64_t* rows, int32_t nlists,
  *                         (app/ml/embeddings.py:101-105, modeling_clip.py:683-717)
  *   MRAG_ENC_BERT         replaces SentenceTransformer(all-MiniLM-L6-v2).encode =
  *                         BertModel + mean pooling (app/ml/embeddings.py:62-68)
+ *   MRAG_ENC_BERT_PAIR    replaces CrossEncoder(ms-marco-MiniLM-L-6-v2).predict =
+ *                         BertForSequenceClassification on (query, passage) pairs
+ *                         (app/ml/retrieve.py:29-38, 132-155; modeling_bert.py pooler +
+ *                         classifier); parameters under their "bert." / "classifier." names
  * Parameters are set by Hugging Face state-dict name (f32 host arrays, e.g.
  * "vision_model.encoder.layers.0.self_attn.q_proj.weight"); compute is fp16 MFMA
  * GEMMs with f32 accumulation and an f32 residual stream. With normalize != 0 the
@@ -134,6 +138,7 @@ int mrag_topk_merge(const double* scores64, const int64_t* rows, int32_t nlists,
 #define MRAG_ENC_CLIP_VISION 1
 #define MRAG_ENC_CLIP_TEXT 2
 #define MRAG_ENC_BERT 3
+#define MRAG_ENC_BERT_PAIR 4
 
 typedef struct mrag_encoder_config {
   int32_t kind;           /* MRAG_ENC_*                                            */
@@ -143,7 +148,7 @@ typedef struct mrag_encoder_config {
   int32_t intermediate;   /* 3072, 2048, 1536                                      */
   int32_t max_positions;  /* text: 77 / 512; vision: unused                        */
   int32_t vocab;          /* text: 49408 / 30522                                   */
-  int32_t proj_dim;       /* CLIP: 512; BERT: unused                               */
+  int32_t proj_dim;       /* CLIP: 512; BERT: unused; BERT_PAIR: num_labels (1)    */
   int32_t image_size;     /* vision: 224                                           */
   int32_t patch_size;     /* vision: 32                                            */
   int32_t act;            /* 0 = quick_gelu (CLIP), 1 = gelu (erf, BERT)          */
@@ -169,6 +174,13 @@ int mrag_encoder_embed_images(mrag_encoder* enc, const uint8_t* images, int32_t 
  * mean-pooled over the mask). */
 int mrag_encoder_embed_tokens(mrag_encoder* enc, const int32_t* ids, const int32_t* mask, int32_t batch,
                               int32_t seq, float* out, int32_t normalize, int32_t ptr_kind, void* stream);
+
+/* Cross-encoder (MRAG_ENC_BERT_PAIR): ids / token_type_ids / attention mask int32
+ * [batch][seq] ("[CLS] a [SEP] b [SEP]", types 0 / 1; type_ids or mask may be NULL =
+ * zeros / ones), seq <= max_positions (512) -> out f32 [batch][num_labels] logits
+ * (before any activation). */
+int mrag_encoder_score_pairs(mrag_encoder* enc, const int32_t* ids, const int32_t* type_ids, const int32_t* mask,
+                             int32_t batch, int32_t seq, float* out, int32_t ptr_kind, void* stream);
 
 /* K0: image resize (shortest edge -> size, bicubic) + centre crop, bit-exact to the
  * reference's preprocessing (CLIPImageProcessor -> PIL.Image.resize(BICUBIC) + center_crop,

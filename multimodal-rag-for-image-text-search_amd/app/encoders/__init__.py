@@ -21,6 +21,7 @@ from app.encoders.weights import (
     CLIP_TEXT_B32,
     CLIP_VISION_B32,
     MINILM_L6,
+    MSMARCO_MINILM_L6_CE,
     EncoderConfig,
     checkpoint_state_dict,
     param_specs,
@@ -45,6 +46,7 @@ def _register_signatures():
         "mrag_encoder_embed_images": [vp, vp, i32, vp, i32, i32, vp],
         "mrag_encoder_embed_tokens": [vp, vp, vp, i32, i32, vp, i32, i32, vp],
         "mrag_gemm_nt": [vp, vp, vp, vp, i32, i32, i32, i32, vp],
+        "mrag_encoder_score_pairs": [vp, vp, vp, vp, i32, i32, vp, i32, vp],
     }
     for name, args in sigs.items():
         fn = getattr(lib, name)
@@ -149,6 +151,23 @@ class GpuEncoder:
         _native.check(self.lib.mrag_encoder_embed_tokens(self._h, i.ctypes.data, m.ctypes.data if m is not None else None,
                                                          i.shape[0], i.shape[1], out.ctypes.data, int(normalize),
                                                          _native.MRAG_PTR_HOST, None), "embed_tokens")
+        return out
+
+
+    def score_pairs(self, ids, type_ids=None, mask=None):
+        """Cross-encoder logits: ids / type_ids / mask int [B, T] host arrays -> f32 [B, num_labels]."""
+        if self.cfg.kind != 4:
+            raise TypeError("not a cross-encoder")
+        i = np.ascontiguousarray(ids, dtype=np.int32)
+        if i.ndim != 2:
+            raise ValueError("ids must be [B, T]")
+        t = np.ascontiguousarray(type_ids, dtype=np.int32) if type_ids is not None else None
+        m = np.ascontiguousarray(mask, dtype=np.int32) if mask is not None else None
+        out = np.empty((i.shape[0], self.cfg.proj_dim), dtype=np.float32)
+        _native.check(self.lib.mrag_encoder_score_pairs(self._h, i.ctypes.data, t.ctypes.data if t is not None else None,
+                                                        m.ctypes.data if m is not None else None, i.shape[0],
+                                                        i.shape[1], out.ctypes.data, _native.MRAG_PTR_HOST, None),
+                      "score_pairs")
         return out
 
 

@@ -14,7 +14,7 @@ from __future__ import annotations
 
 import json
 import os
-from typing import Optional, Sequence
+from typing import Optional, Sequence, Tuple
 
 import numpy as np
 
@@ -143,3 +143,69 @@ class ClipProcessor:
             ids, mask = self.tokenizer(list(text))
             return BatchInputs(input_ids=ids, attention_mask=mask)
         raise ValueError("ClipProcessor needs images= or text=")
+
+
+class CrossEncoderModel:
+    """GPU stand-in for ``sentence_transformers.CrossEncoder`` as the reference uses it
+    (``CrossEncoder(settings.models.reranker).predict(pairs)``, app/ml/retrieve.py:29-38,
+    148): BertForSequenceClassification (MRAG_ENC_BERT_PAIR: BERT-6L/384 on the MiniLM
+    kernels + [CLS] pooler + classifier) on "[CLS] query [SEP] passage [SEP]" pairs.
+
+    ``predict`` restates sentence-transformers' (unpinned, not installed) semantics:
+    batches of ``batch_size`` pairs, tokenizer truncation 'longest_first' to
+    ``max_length`` (512 = the model's positions), logits -> activation -> for one label
+    a float32 vector (a scalar for a single pair). The default activation comes from the
+    checkpoint's ``config.json`` key ``sbert_ce_default_activation_function`` (the
+    ms-marco cross-encoders set Identity: raw logits) and otherwise is Sigmoid for one
+    label / Identity for several — sentence-transformers' rule."""
+
+    def __init__(self, model_name_or_path: Optional[str] = None, max_length: Optional[int] = None,
+                 device: Optional[int] = None, seed: int = 0):
+        from app.encoders.weights import MSMARCO_MINILM_L6_CE
+
+        d = _local_dir(model_name_or_path)
+        self.device = _device_index() if device is None else device
+        self.cfg = MSMARCO_MINILM_L6_CE
+        self.enc = load_encoder(self.cfg, d, device=self.device, seed=seed)
+        self.tokenizer = WordPieceTokenizer(d, max_len=max_length or self.cfg.max_positions)
+        self.num_labels = self.cfg.proj_dim
+        act = None
+        if d and os.path.exists(os.path.join(d, "config.json")):
+            with open(os.path.join(d, "config.json")) as f:
+                act = json.load(f).get("sbert_ce_default_activation_function")
+        if act is not None:
+            self.activation = "identity" if act.endswith("Identity") else ("sigmoid" if act.endswith("Sigmoid") else act)
+        else:
+            self.activation = "sigmoid" if self.num_labels == 1 else "identity"
+
+    def to(self, device):
+        return self
+
+    def logits(self, pairs: Sequence[Tuple[str, str]], batch_size: int = 32) -> np.ndarray:
+        out = []
+        for i in range(0, len(pairs), batch_size):
+            ids, types, mask = self.tokenizer.pairs(pairs[i:i + batch_size])
+            out.append(self.enc.score_pairs(ids, types, mask))
+        return np.concatenate(out) if out else np.empty((0, self.num_labels), dtype=np.float32)
+
+    def predict(self, sentences, batch_size: int = 32, show_progress_bar=None, activation_fct=None,
+                apply_softmax: bool = False, convert_to_numpy: bool = True, convert_to_tensor: bool = False, **kw):
+        single = len(sentences) > 0 and isinstance(sentences[0], str)
+        pairs = [tuple(sentences)] if single else [tuple(p) for p in sentences]
+        z = self.logits(pairs, batch_size)
+        if activation_fct is not None:
+            import torch
+
+            z = activation_fct(torch.from_numpy(z)).numpy()
+        elif self.activation == "sigmoid":
+            z = (1.0 / (1.0 + np.exp(-z.astype(np.float64)))).astype(np.float32)
+        if apply_softmax and z.shape[1] > 1:
+            e = np.exp(z - z.max(axis=1, keepdims=True))
+            z = e / e.sum(axis=1, keepdims=True)
+        scores = z[:, 0] if self.num_labels == 1 else z
+        scores = np.asarray(scores, dtype=np.float32)
+        if convert_to_tensor:
+            import torch
+
+            scores = torch.from_numpy(scores)
+        return scores[0] if single else scores

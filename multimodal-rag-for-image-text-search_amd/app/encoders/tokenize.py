@@ -49,7 +49,8 @@ class WordPieceTokenizer:
         if model_dir and os.path.exists(os.path.join(model_dir, "vocab.txt")):
             from tokenizers import BertWordPieceTokenizer
 
-            self._tok = BertWordPieceTokenizer(os.path.join(model_dir, "vocab.txt"), lowercase=True)
+            self._vocab_path = os.path.join(model_dir, "vocab.txt")
+            self._tok = BertWordPieceTokenizer(self._vocab_path, lowercase=True)
 
     def encode_one(self, text: str) -> List[int]:
         if self._tok is not None:
@@ -69,6 +70,46 @@ class WordPieceTokenizer:
             ids[i, : len(s)] = s
             mask[i, : len(s)] = 1
         return ids, mask
+
+    def _body(self, text: str) -> List[int]:
+        if self._tok is not None:
+            return self._tok.encode(text, add_special_tokens=False).ids
+        return [_hash_id(t, 1000, self.vocab) for t in _basic_tokens(text)]
+
+    def encode_pair(self, a: str, b: str) -> Tuple[List[int], List[int]]:
+        """[CLS] a [SEP] b [SEP] with token types 0 / 1, truncated 'longest_first' (one
+        token at a time from the longer side) to max_len — the HF tokenizer's
+        truncation=True for pairs, as CrossEncoder.predict calls it."""
+        if self._tok is not None:
+            if getattr(self, "_pair_tok", None) is None:
+                from tokenizers import BertWordPieceTokenizer
+
+                self._pair_tok = BertWordPieceTokenizer(self._vocab_path, lowercase=True)
+                self._pair_tok.enable_truncation(max_length=self.max_len, strategy="longest_first")
+            enc = self._pair_tok.encode(a, b)
+            return list(enc.ids), list(enc.type_ids)
+        x, y = self._body(a), self._body(b)
+        budget = self.max_len - 3
+        while len(x) + len(y) > budget:
+            if len(x) > len(y):
+                x.pop()
+            else:
+                y.pop()
+        ids = [self.CLS] + x + [self.SEP] + y + [self.SEP]
+        types = [0] * (len(x) + 2) + [1] * (len(y) + 1)
+        return ids, types
+
+    def pairs(self, pairs: Sequence[Tuple[str, str]]) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+        enc = [self.encode_pair(a, b) for a, b in pairs]
+        T = max(len(i) for i, _ in enc)
+        ids = np.full((len(enc), T), self.PAD, dtype=np.int32)
+        types = np.zeros((len(enc), T), dtype=np.int32)
+        mask = np.zeros((len(enc), T), dtype=np.int32)
+        for r, (i, t) in enumerate(enc):
+            ids[r, : len(i)] = i
+            types[r, : len(t)] = t
+            mask[r, : len(i)] = 1
+        return ids, types, mask
 
 
 class ClipTokenizer:

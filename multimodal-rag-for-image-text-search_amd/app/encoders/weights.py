@@ -25,7 +25,7 @@ import numpy as np
 
 @dataclass(frozen=True)
 class EncoderConfig:
-    kind: int  # 1 CLIP vision, 2 CLIP text, 3 BERT
+    kind: int  # 1 CLIP vision, 2 CLIP text, 3 BERT, 4 BERT pair classifier (cross-encoder)
     hidden: int
     layers: int
     heads: int
@@ -49,6 +49,10 @@ CLIP_TEXT_B32 = EncoderConfig(kind=2, hidden=512, layers=12, heads=8, intermedia
 # all-MiniLM-L6-v2 = BertModel(hidden 384, 6 layers, 12 heads, intermediate 1536)
 MINILM_L6 = EncoderConfig(kind=3, hidden=384, layers=6, heads=12, intermediate=1536, max_positions=512,
                           vocab=30522, act=1, ln_eps=1e-12)
+# cross-encoder/ms-marco-MiniLM-L-6-v2 (the reference's RERANKER_MODEL default) =
+# BertForSequenceClassification(MiniLM-L6 dims, num_labels = 1); proj_dim carries num_labels
+MSMARCO_MINILM_L6_CE = EncoderConfig(kind=4, hidden=384, layers=6, heads=12, intermediate=1536, max_positions=512,
+                                     vocab=30522, proj_dim=1, act=1, ln_eps=1e-12)
 
 
 def param_specs(cfg: EncoderConfig) -> List[Tuple[str, Tuple[int, ...], str]]:
@@ -92,15 +96,21 @@ def param_specs(cfg: EncoderConfig) -> List[Tuple[str, Tuple[int, ...], str]]:
                 ("text_projection.weight", (cfg.proj_dim, D), "linear"),
             ]
     else:
+        b = "bert." if cfg.kind == 4 else ""  # BertForSequenceClassification wraps BertModel as .bert
         out += [
-            ("embeddings.word_embeddings.weight", (cfg.vocab, D), "emb"),
-            ("embeddings.position_embeddings.weight", (cfg.max_positions, D), "emb"),
-            ("embeddings.token_type_embeddings.weight", (2, D), "emb"),
-            ("embeddings.LayerNorm.weight", (D,), "ln_w"),
-            ("embeddings.LayerNorm.bias", (D,), "ln_b"),
+            (b + "embeddings.word_embeddings.weight", (cfg.vocab, D), "emb"),
+            (b + "embeddings.position_embeddings.weight", (cfg.max_positions, D), "emb"),
+            (b + "embeddings.token_type_embeddings.weight", (2, D), "emb"),
+            (b + "embeddings.LayerNorm.weight", (D,), "ln_w"),
+            (b + "embeddings.LayerNorm.bias", (D,), "ln_b"),
         ]
+        if cfg.kind == 4:
+            out += [
+                ("bert.pooler.dense.weight", (D, D), "linear"), ("bert.pooler.dense.bias", (D,), "bias"),
+                ("classifier.weight", (cfg.proj_dim, D), "linear"), ("classifier.bias", (cfg.proj_dim,), "bias"),
+            ]
         for i in range(cfg.layers):
-            l = f"encoder.layer.{i}."
+            l = f"{b}encoder.layer.{i}."
             for p in ("query", "key", "value"):
                 out += [(l + f"attention.self.{p}.weight", (D, D), "linear"), (l + f"attention.self.{p}.bias", (D,), "bias")]
             out += [
@@ -172,7 +182,7 @@ def checkpoint_state_dict(path: str, cfg: EncoderConfig) -> Optional[Dict[str, n
     out: Dict[str, np.ndarray] = {}
     for f in sorted(files):
         for k, v in load_file(os.path.join(path, f)).items():
-            for cand in (k, k.replace("0.auto_model.", ""), k.replace("bert.", "")):
+            for cand in (k, k.replace("0.auto_model.", ""), k.replace("bert.", ""), "bert." + k):
                 if cand in want:
                     out[cand] = np.asarray(v, dtype=np.float32)
     missing = want - set(out)

@@ -7,9 +7,10 @@ order. ``retrieve`` (:103-117): optional cross-encoder rerank + z-score fusion
 ``embed_text_batch``, ``embed_query_for_images``, ``_get_cross_encoder``,
 ``get_index_version`` are looked up at call time (test seams, tests/test_retrieve.py).
 
-The cross-encoder (ms-marco-MiniLM-L-6, a name-based hub download) is unavailable
-offline, so ``_get_cross_encoder`` returns False exactly as the reference does when the
-load fails (:29-38) and rerank is skipped. For many queries at once use
+The cross-encoder (ms-marco-MiniLM-L-6) runs on the GPU (``CrossEncoderModel``,
+MRAG_ENC_BERT_PAIR) when RERANKER_MODEL is a local checkpoint directory (or
+MRAG_SYNTHETIC_RERANKER=1); a hub name offline returns False exactly as the reference
+does when the load fails (:29-38), and rerank is skipped. For many queries at once use
 ``app.retrieval`` (batched GPU search).
 """
 from __future__ import annotations
@@ -43,8 +44,23 @@ def _get_cross_encoder():
 
             _CROSS_ENCODER = CrossEncoder(settings.models.reranker)
         except Exception:
-            _CROSS_ENCODER = False
+            _CROSS_ENCODER = _gpu_cross_encoder()
     return _CROSS_ENCODER
+
+
+def _gpu_cross_encoder():
+    """The GPU cross-encoder when its weights exist locally (RERANKER_MODEL = a checkpoint
+    directory) or synthetic weights are requested (MRAG_SYNTHETIC_RERANKER=1, benchmarks /
+    tests); otherwise False — the reference's outcome when the hub model cannot load."""
+    name = settings.models.reranker
+    if not (os.path.isdir(name) or os.environ.get("MRAG_SYNTHETIC_RERANKER") == "1"):
+        return False
+    try:
+        from app.encoders.models import CrossEncoderModel
+
+        return CrossEncoderModel(name)
+    except Exception:
+        return False
 
 
 def _prepare_metadata(chunk: Chunk) -> Dict[str, Any]:

@@ -3,6 +3,8 @@
 //   MRAG_ENC_CLIP_TEXT    CLIPModel.get_text_features   (app/ml/embeddings.py:101-105)
 //   MRAG_ENC_BERT         SentenceTransformer(all-MiniLM-L6-v2).encode: BERT + mean pool
 //                         (app/ml/embeddings.py:62-70)
+//   MRAG_ENC_BERT_PAIR    CrossEncoder(ms-marco-MiniLM-L-6-v2).predict logits:
+//                         BertForSequenceClassification (app/ml/retrieve.py:132-155)
 // Parameters arrive under their Hugging Face state-dict names (f32 host arrays) and are
 // packed once into device buffers: f16 GEMM weights with q|k|v fused into one [3D][D]
 // matrix, f32 biases / LayerNorm params / embeddings. A forward is ~7 launches per layer
@@ -61,11 +63,12 @@ struct mrag_encoder {
   std::vector<Layer> layers;
   // embeddings / heads
   Buf patch_w, cls, pos, pre_g, pre_b, post_g, post_b, proj_w;  // vision
-  Buf tok, type0, emb_g, emb_b;                                  // text / bert (+pos)
+  Buf tok, type0, emb_g, emb_b;                                  // text / bert (+pos); type0 = [2][D]
+  Buf pool_w, pool_b, cls_w, cls_b, POOL32;                      // bert pair: pooler + classifier
   std::map<std::string, bool> loaded;
   std::vector<std::string> expected;
   // workspace
-  Buf X, H16, QKV, ATT, F16, PATCH, IMG, IDS, MASK, ROWS, POOL16, OUT;
+  Buf X, H16, QKV, ATT, F16, PATCH, IMG, IDS, MASK, TYPES, ROWS, POOL16, OUT;
   int64_t ws_tokens = 0;
 };
 
@@ -150,12 +153,18 @@ std::vector<std::string> expected_names(const mrag_encoder_config& c) {
         v.push_back(l + n);
     }
   } else {
+    // BertModel names (sentence-transformers checkpoint) or "bert."-prefixed ones under
+    // BertForSequenceClassification (the cross-encoder)
+    const std::string pre = c.kind == MRAG_ENC_BERT_PAIR ? "bert." : "";
     for (const char* n : {"embeddings.word_embeddings.weight", "embeddings.position_embeddings.weight",
                           "embeddings.token_type_embeddings.weight", "embeddings.LayerNorm.weight",
                           "embeddings.LayerNorm.bias"})
-      v.push_back(n);
+      v.push_back(pre + n);
+    if (c.kind == MRAG_ENC_BERT_PAIR)
+      for (const char* n : {"bert.pooler.dense.weight", "bert.pooler.dense.bias", "classifier.weight", "classifier.bias"})
+        v.push_back(n);
     for (int i = 0; i < c.layers; ++i) {
-      const std::string l = "encoder.layer." + std::to_string(i) + ".";
+      const std::string l = pre + "encoder.layer." + std::to_string(i) + ".";
       for (const char* n : {"attention.self.query.weight", "attention.self.query.bias", "attention.self.key.weight",
                             "attention.self.key.bias", "attention.self.value.weight", "attention.self.value.bias",
                             "attention.output.dense.weight", "attention.output.dense.bias",
@@ -175,6 +184,9 @@ int64_t expected_numel(const mrag_encoder_config& c, const std::string& name) {
     return name.size() >= n && name.compare(name.size() - n, n, suf) == 0;
   };
   if (ends("class_embedding")) return D;
+  if (ends("pooler.dense.weight")) return D * D;
+  if (ends("classifier.weight")) return (int64_t)c.proj_dim * D;
+  if (ends("classifier.bias")) return c.proj_dim;
   if (ends("patch_embedding.weight")) return D * 3 * c.patch_size * c.patch_size;
   if (ends("embeddings.position_embedding.weight") || ends("position_embeddings.weight")) {
     if (c.kind == MRAG_ENC_CLIP_VISION) {
@@ -219,6 +231,8 @@ int ensure_workspace(mrag_encoder* e, int B, int T) {
   }
   if (int rc = buf_ensure(e->ROWS, (size_t)B * 4 + 256)) return rc;
   if (int rc = buf_ensure(e->POOL16, (size_t)B * D * 2)) return rc;
+  if (c.kind == MRAG_ENC_BERT_PAIR)
+    if (int rc = buf_ensure(e->POOL32, (size_t)B * D * 4)) return rc;
   e->ws_tokens = tokens;
   return MRAG_OK;
 }
@@ -320,7 +334,8 @@ int mrag_encoder_create(const mrag_encoder_config* cfg, int32_t device, mrag_enc
   MRAG_REQUIRE(cfg && out, "NULL argument");
   *out = nullptr;
   const auto& c = *cfg;
-  MRAG_REQUIRE(c.kind == MRAG_ENC_CLIP_VISION || c.kind == MRAG_ENC_CLIP_TEXT || c.kind == MRAG_ENC_BERT,
+  MRAG_REQUIRE(c.kind == MRAG_ENC_CLIP_VISION || c.kind == MRAG_ENC_CLIP_TEXT || c.kind == MRAG_ENC_BERT ||
+                   c.kind == MRAG_ENC_BERT_PAIR,
                "unknown encoder kind %d", c.kind);
   MRAG_REQUIRE(c.hidden > 0 && c.hidden % 128 == 0 && c.hidden <= 1024, "hidden %d unsupported (multiple of 128, <= 1024)",
                c.hidden);
@@ -330,7 +345,9 @@ int mrag_encoder_create(const mrag_encoder_config* cfg, int32_t device, mrag_enc
                "head_dim must be 32 or 64");
   MRAG_REQUIRE(c.layers >= 1 && c.layers <= 64, "layers %d", c.layers);
   MRAG_REQUIRE(c.act == 0 || c.act == 1, "act %d", c.act);
-  if (c.kind != MRAG_ENC_BERT) MRAG_REQUIRE(c.proj_dim % 128 == 0 && c.proj_dim > 0, "proj_dim must be a multiple of 128");
+  if (c.kind == MRAG_ENC_CLIP_VISION || c.kind == MRAG_ENC_CLIP_TEXT)
+    MRAG_REQUIRE(c.proj_dim % 128 == 0 && c.proj_dim > 0, "proj_dim must be a multiple of 128");
+  if (c.kind == MRAG_ENC_BERT_PAIR) MRAG_REQUIRE(c.proj_dim >= 1 && c.proj_dim <= 64, "num_labels %d", c.proj_dim);
   if (c.kind == MRAG_ENC_CLIP_VISION)
     MRAG_REQUIRE(c.patch_size > 0 && c.image_size % c.patch_size == 0 && (3 * c.patch_size * c.patch_size) % 64 == 0 &&
                      c.patch_size % 8 == 0,
@@ -363,7 +380,8 @@ int mrag_encoder_destroy(mrag_encoder* e) {
         buf_free(*b);
     for (Buf* b : {&e->patch_w, &e->cls, &e->pos, &e->pre_g, &e->pre_b, &e->post_g, &e->post_b, &e->proj_w, &e->tok,
                    &e->type0, &e->emb_g, &e->emb_b, &e->X, &e->H16, &e->QKV, &e->ATT, &e->F16, &e->PATCH, &e->IMG,
-                   &e->IDS, &e->MASK, &e->ROWS, &e->POOL16, &e->OUT})
+                   &e->IDS, &e->MASK, &e->ROWS, &e->POOL16, &e->OUT, &e->pool_w, &e->pool_b, &e->cls_w, &e->cls_b,
+                   &e->POOL32, &e->TYPES})
       buf_free(*b);
     (void)hipStreamDestroy(e->stream);
   }
@@ -390,7 +408,8 @@ int mrag_encoder_set_param(mrag_encoder* e, const char* cname, const float* data
     return name.size() >= n && name.compare(name.size() - n, n, suf) == 0;
   };
   int rc = MRAG_OK;
-  const int li = c.kind == MRAG_ENC_BERT ? layer_index(name, "encoder.layer.") : layer_index(name, "encoder.layers.");
+  const bool bert = c.kind == MRAG_ENC_BERT || c.kind == MRAG_ENC_BERT_PAIR;
+  const int li = bert ? layer_index(name, "encoder.layer.") : layer_index(name, "encoder.layers.");
   if (li >= 0) {
     MRAG_REQUIRE(li < c.layers, "layer index %d out of range", li);
     Layer& L = e->layers[li];
@@ -425,7 +444,15 @@ int mrag_encoder_set_param(mrag_encoder* e, const char* cname, const float* data
   } else if (ends("token_embedding.weight") || ends("word_embeddings.weight")) {
     rc = upload(e->tok, data, numel, false, s);
   } else if (ends("token_type_embeddings.weight")) {
-    rc = upload(e->type0, data, D, false, s);  // row 0 only (token_type_ids == 0)
+    rc = upload(e->type0, data, numel, false, s);  // [2][D]; single-text BERT reads row 0
+  } else if (ends("pooler.dense.weight")) {
+    rc = upload(e->pool_w, data, numel, true, s);
+  } else if (ends("pooler.dense.bias")) {
+    rc = upload(e->pool_b, data, numel, false, s);
+  } else if (ends("classifier.weight")) {
+    rc = upload(e->cls_w, data, numel, false, s);
+  } else if (ends("classifier.bias")) {
+    rc = upload(e->cls_b, data, numel, false, s);
   } else if (ends("pre_layrnorm.weight")) {
     rc = upload(e->pre_g, data, numel, false, s);
   } else if (ends("pre_layrnorm.bias")) {
@@ -545,8 +572,8 @@ int mrag_encoder_embed_tokens(mrag_encoder* e, const int32_t* ids, const int32_t
     dst = (float*)e->OUT.p;
   }
   if (c.kind == MRAG_ENC_CLIP_TEXT) {
-    if (int rc = launch_token_embed(dids, (const float*)e->tok.p, (const float*)e->pos.p, nullptr, X, B, T, D, c.vocab,
-                                    s))
+    if (int rc = launch_token_embed(dids, (const float*)e->tok.p, (const float*)e->pos.p, nullptr, nullptr, X, B, T, D,
+                                    c.vocab, s))
       return rc;
     for (int i = 0; i < c.layers; ++i)
       if (int rc = clip_layer(e, e->layers[i], B, T, dmask, 1, s)) return rc;
@@ -556,8 +583,8 @@ int mrag_encoder_embed_tokens(mrag_encoder* e, const int32_t* ids, const int32_t
       return rc;
     if (int rc = gemm(e->POOL16.p, e->proj_w.p, nullptr, dst, B, c.proj_dim, D, c.proj_dim, EPI_F32, s)) return rc;
   } else {
-    if (int rc = launch_token_embed(dids, (const float*)e->tok.p, (const float*)e->pos.p, (const float*)e->type0.p, X,
-                                    B, T, D, c.vocab, s))
+    if (int rc = launch_token_embed(dids, (const float*)e->tok.p, (const float*)e->pos.p, (const float*)e->type0.p,
+                                    nullptr, X, B, T, D, c.vocab, s))
       return rc;
     if (int rc = layernorm(X, nullptr, X, H, e->emb_g, e->emb_b, B * T, D, c.ln_eps, s)) return rc;
     for (int i = 0; i < c.layers; ++i)
@@ -567,6 +594,75 @@ int mrag_encoder_embed_tokens(mrag_encoder* e, const int32_t* ids, const int32_t
   if (normalize)
     if (int rc = mrag_l2norm_rows(dst, dst, B, outD, s)) return rc;
   if (ptr_kind == MRAG_PTR_HOST) MRAG_HIP(hipMemcpyAsync(out, dst, (size_t)B * outD * 4, hipMemcpyDeviceToHost, s));
+  MRAG_HIP(hipStreamSynchronize(s));
+  return MRAG_OK;
+}
+
+int mrag_encoder_score_pairs(mrag_encoder* e, const int32_t* ids, const int32_t* type_ids, const int32_t* mask,
+                             int32_t batch, int32_t seq, float* out, int32_t ptr_kind, void* stream_arg) {
+  MRAG_REQUIRE(e != nullptr, "NULL encoder");
+  MRAG_REQUIRE(e->cfg.kind == MRAG_ENC_BERT_PAIR, "not a cross-encoder (MRAG_ENC_BERT_PAIR)");
+  MRAG_REQUIRE(batch >= 0 && seq >= 1, "bad shape batch=%d seq=%d", batch, seq);
+  MRAG_REQUIRE(seq <= e->cfg.max_positions && seq <= 512, "seq %d exceeds max positions (%d) or 512", seq,
+               e->cfg.max_positions);
+  MRAG_REQUIRE(ptr_kind == MRAG_PTR_HOST || ptr_kind == MRAG_PTR_DEVICE, "bad ptr_kind");
+  std::lock_guard<std::mutex> lk(e->mu);
+  mrag::DeviceGuard g(e->device);
+  if (int rc = check_ready(e)) return rc;
+  if (batch == 0) return MRAG_OK;
+  MRAG_REQUIRE(ids && out, "NULL ids/out");
+  hipStream_t s = stream_arg ? (hipStream_t)stream_arg : e->stream;
+  const auto& c = e->cfg;
+  const int B = batch, T = seq, D = c.hidden, NL = c.proj_dim;
+  if (int rc = ensure_workspace(e, B, T)) return rc;
+  const int32_t* dids = ids;
+  const int32_t* dmask = mask;
+  const int32_t* dtypes = type_ids;
+  if (ptr_kind == MRAG_PTR_HOST) {
+    if (int rc = buf_ensure(e->IDS, (size_t)B * T * 4)) return rc;
+    MRAG_HIP(hipMemcpyAsync(e->IDS.p, ids, (size_t)B * T * 4, hipMemcpyHostToDevice, s));
+    dids = (const int32_t*)e->IDS.p;
+    if (mask) {
+      if (int rc = buf_ensure(e->MASK, (size_t)B * T * 4)) return rc;
+      MRAG_HIP(hipMemcpyAsync(e->MASK.p, mask, (size_t)B * T * 4, hipMemcpyHostToDevice, s));
+      dmask = (const int32_t*)e->MASK.p;
+    }
+    if (type_ids) {
+      if (int rc = buf_ensure(e->TYPES, (size_t)B * T * 4)) return rc;
+      MRAG_HIP(hipMemcpyAsync(e->TYPES.p, type_ids, (size_t)B * T * 4, hipMemcpyHostToDevice, s));
+      dtypes = (const int32_t*)e->TYPES.p;
+    }
+  }
+  float* X = (float*)e->X.p;
+  _Float16* H = (_Float16*)e->H16.p;
+  if (int rc = launch_token_embed(dids, (const float*)e->tok.p, (const float*)e->pos.p, (const float*)e->type0.p, dtypes,
+                                  X, B, T, D, c.vocab, s))
+    return rc;
+  if (int rc = layernorm(X, nullptr, X, H, e->emb_g, e->emb_b, B * T, D, c.ln_eps, s)) return rc;
+  for (int i = 0; i < c.layers; ++i)
+    if (int rc = bert_layer(e, e->layers[i], B, T, dmask, s)) return rc;
+  // pooler: dense over the [CLS] rows (token 0 of each sequence: A rows strided by T*D)
+  GemmArgs pg{};
+  pg.A = H;
+  pg.W = (const _Float16*)e->pool_w.p;
+  pg.bias = (const float*)e->pool_b.p;
+  pg.C = e->POOL32.p;
+  pg.M = B;
+  pg.N = D;
+  pg.K = D;
+  pg.lda = T * D;
+  pg.ldw = D;
+  pg.ldc = D;
+  if (int rc = launch_gemm(pg, EPI_F32, s)) return rc;
+  float* dst = out;
+  if (ptr_kind == MRAG_PTR_HOST) {
+    if (int rc = buf_ensure(e->OUT, (size_t)B * NL * 4)) return rc;
+    dst = (float*)e->OUT.p;
+  }
+  if (int rc = launch_cls_head((const float*)e->POOL32.p, (const float*)e->cls_w.p, (const float*)e->cls_b.p, dst, B, D,
+                               NL, s))
+    return rc;
+  if (ptr_kind == MRAG_PTR_HOST) MRAG_HIP(hipMemcpyAsync(out, dst, (size_t)B * NL * 4, hipMemcpyDeviceToHost, s));
   MRAG_HIP(hipStreamSynchronize(s));
   return MRAG_OK;
 }

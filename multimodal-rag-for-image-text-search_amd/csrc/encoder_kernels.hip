@@ -10,6 +10,7 @@
 // Layout: activations row-major [tokens][features]; the residual stream is f32, every GEMM
 // input is f16 (LayerNorm writes the f16 copy), weights are f16 [out][in] (torch Linear
 // layout, K contiguous for both GEMM operands), biases / LN params / embeddings f32.
+#include <algorithm>
 #include <cstdlib>
 
 #include "common.h"
@@ -324,9 +325,10 @@ __global__ __launch_bounds__(256) void layernorm_kernel(LayerNormArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// K4: multi-head attention for short sequences (L <= 256): one workgroup per
-// (sequence, head), K and V of the head in LDS (f32), one thread per query row with
-// an online softmax over the keys (key padding mask, optional causal mask).
+// K4: multi-head attention for sequences up to 512 (K and V of the head f32 in LDS:
+// 2 L dh 4 bytes <= 160 KiB): one workgroup per (sequence, head), each thread takes query
+// rows i, i + blockDim, ... with an online softmax over the keys (key padding mask,
+// optional causal mask).
 // qkv: [B*L][3*D] f16 (q | k | v, head h at columns h*DH), out: [B*L][D] f16.
 template <int DH>
 __global__ __launch_bounds__(256) void attention_kernel(AttentionArgs a) {
@@ -345,8 +347,7 @@ __global__ __launch_bounds__(256) void attention_kernel(AttentionArgs a) {
   }
   for (int t = threadIdx.x; t < a.L; t += blockDim.x) valid[t] = a.mask ? (a.mask[b * a.L + t] != 0) : 1;
   __syncthreads();
-  const int i = threadIdx.x;
-  if (i >= a.L) return;
+  for (int i = threadIdx.x; i < a.L; i += blockDim.x) {
   float q[DH], o[DH];
   const _Float16* qr = base + i * rs + hd * DH;
 #pragma unroll
@@ -375,6 +376,7 @@ __global__ __launch_bounds__(256) void attention_kernel(AttentionArgs a) {
   _Float16* orow = a.out + ((size_t)b * a.L + i) * D + hd * DH;
 #pragma unroll
   for (int d = 0; d < DH; ++d) orow[d] = (_Float16)(o[d] * inv);
+  }
 }
 
 // K4 (MFMA form) for L <= 64, head_dim 64 — the ViT-B/32 case (L = 50) and short text.
@@ -552,8 +554,9 @@ __global__ void vit_assemble_kernel(const float* __restrict__ patch, const float
 
 // Token embeddings: X[b*T+t] = tok[ids] + pos[t] (+ type0 for BERT)   (f32)
 __global__ void token_embed_kernel(const int32_t* __restrict__ ids, const float* __restrict__ tok,
-                                   const float* __restrict__ pos, const float* __restrict__ type0,
-                                   float* __restrict__ X, int B, int T, int D, int vocab) {
+                                   const float* __restrict__ pos, const float* __restrict__ type_tab,
+                                   const int32_t* __restrict__ types, float* __restrict__ X, int B, int T, int D,
+                                   int vocab) {
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= (int64_t)B * T * D) return;
   const int d = (int)(idx % D);
@@ -562,7 +565,7 @@ __global__ void token_embed_kernel(const int32_t* __restrict__ ids, const float*
   int id = ids[bt];
   id = id < 0 ? 0 : (id >= vocab ? vocab - 1 : id);
   float e = tok[(size_t)id * D + d] + pos[(size_t)t * D + d];
-  if (type0) e += type0[d];
+  if (type_tab) e += type_tab[(types ? (types[bt] != 0) : 0) * D + d];  // BERT type_vocab_size 2
   X[idx] = e;
 }
 
@@ -681,10 +684,10 @@ bool force_valu_attention() {
 
 int launch_attention(const AttentionArgs& a, int dh, hipStream_t s) {
   if (a.B <= 0) return MRAG_OK;
-  MRAG_REQUIRE(a.L >= 1 && a.L <= 256, "attention: L=%d unsupported (1..256)", a.L);
+  MRAG_REQUIRE(a.L >= 1 && a.L <= 512, "attention: L=%d unsupported (1..512)", a.L);
   const size_t shm = (size_t)2 * a.L * dh * 4 + (size_t)a.L * 4;
   MRAG_REQUIRE(shm <= 160 * 1024, "attention: L*dh too large for LDS");
-  const int threads = (a.L + 63) / 64 * 64;
+  const int threads = std::min(256, (a.L + 63) / 64 * 64);
   const dim3 grid((unsigned)(a.B * a.H));
   // K/V of a head stay f32 in LDS; above 64 KiB the kernel must opt in (gfx950: 160 KiB/CU)
   static bool attr_set = false;
@@ -726,12 +729,37 @@ int launch_vit_assemble(const float* patch, const float* cls, const float* pos, 
   return MRAG_OK;
 }
 
-int launch_token_embed(const int32_t* ids, const float* tok, const float* pos, const float* type0, float* X, int B,
-                       int T, int D, int vocab, hipStream_t s) {
+int launch_token_embed(const int32_t* ids, const float* tok, const float* pos, const float* type_tab,
+                       const int32_t* types, float* X, int B, int T, int D, int vocab, hipStream_t s) {
   const int64_t n = (int64_t)B * T * D;
   if (n == 0) return MRAG_OK;
-  hipLaunchKernelGGL(token_embed_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, ids, tok, pos, type0, X,
-                     B, T, D, vocab);
+  hipLaunchKernelGGL(token_embed_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, ids, tok, pos, type_tab,
+                     types, X, B, T, D, vocab);
+  MRAG_CHECK_LAUNCH();
+  return MRAG_OK;
+}
+
+// Sequence-classification head (BertForSequenceClassification): logits[b][j] =
+// sum_d tanh(pooled[b][d]) * Wc[j][d] + bc[j], pooled = the pooler dense output (f32, bias
+// included). One wave per (row, label); f32 throughout.
+__global__ __launch_bounds__(256) void cls_head_kernel(const float* __restrict__ pooled, const float* __restrict__ Wc,
+                                                       const float* __restrict__ bc, float* __restrict__ out, int B,
+                                                       int D, int NL) {
+  const int wv = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (wv >= B * NL) return;
+  const int b = wv / NL, j = wv - (wv / NL) * NL;
+  float acc = 0.f;
+  for (int d = lane; d < D; d += 64) acc = fmaf(tanhf(pooled[(size_t)b * D + d]), Wc[(size_t)j * D + d], acc);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
+  if (lane == 0) out[(size_t)b * NL + j] = acc + bc[j];
+}
+
+int launch_cls_head(const float* pooled, const float* Wc, const float* bc, float* out, int B, int D, int NL,
+                    hipStream_t s) {
+  if (B * NL == 0) return MRAG_OK;
+  hipLaunchKernelGGL(cls_head_kernel, dim3((unsigned)((B * NL + 3) / 4)), dim3(256), 0, s, pooled, Wc, bc, out, B, D,
+                     NL);
   MRAG_CHECK_LAUNCH();
   return MRAG_OK;
 }

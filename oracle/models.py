@@ -92,6 +92,38 @@ def bert_model(seed: int = 0):
     return model
 
 
+def cross_encoder_model(seed: int = 0):
+    """cross-encoder/ms-marco-MiniLM-L-6-v2 architecture: BertForSequenceClassification
+    (BERT-6L/384 + tanh pooler + 1-logit classifier), synthetic weights by name. The
+    reference reaches it through sentence_transformers.CrossEncoder.predict
+    (app/ml/retrieve.py:148), which tokenises the pairs and returns the activated logits."""
+    import torch
+    from transformers import BertConfig, BertForSequenceClassification
+
+    w = weights_module()
+    c = w.MSMARCO_MINILM_L6_CE
+    cfg = BertConfig(vocab_size=c.vocab, hidden_size=c.hidden, num_hidden_layers=c.layers,
+                     num_attention_heads=c.heads, intermediate_size=c.intermediate,
+                     max_position_embeddings=c.max_positions, hidden_act="gelu", layer_norm_eps=c.ln_eps,
+                     num_labels=c.proj_dim)
+    model = BertForSequenceClassification(cfg).eval()
+    sd = {n: torch.from_numpy(a) for n, a in w.synth_state_dict(c, seed)}
+    missing, unexpected = model.load_state_dict(sd, strict=False)
+    assert not unexpected, unexpected
+    assert all("position_ids" in m or "token_type_ids" in m for m in missing), missing
+    return model
+
+
+def cross_encoder_logits(model, ids: np.ndarray, types: np.ndarray, mask: np.ndarray) -> np.ndarray:
+    import torch
+
+    with torch.no_grad():
+        out = model(input_ids=torch.from_numpy(ids.astype(np.int64)),
+                    token_type_ids=torch.from_numpy(types.astype(np.int64)),
+                    attention_mask=torch.from_numpy(mask.astype(np.int64))).logits
+    return out.float().numpy()
+
+
 def clip_image_embeds(model, images_u8: np.ndarray, normalize: bool = True) -> np.ndarray:
     import torch
 
