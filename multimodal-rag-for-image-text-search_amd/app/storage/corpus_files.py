@@ -1,0 +1,122 @@
+"""On-disk corpus format: the persistence half of the Lance tables the reference keeps in
+``LANCEDB_DIR`` (app/storage/lancedb_store.py:33-44 schema, :87-101 upsert = per-row
+``delete(chunk_id == ...)`` then ``add``). SURVEY.md §8f row 2.
+
+One directory per table (``<db>/mrag_tables/<table>/``), append-only:
+
+* ``seg_<k>.f32``      — the segment's rows, fp32 ``[n][dim]`` little-endian, exactly the
+                         (re-normalised) vectors the reference would write to Lance;
+* ``seg_<k>.parquet``  — the row payloads: chunk_id, user_id, document_id, modality, meta
+                         (JSON text), one Arrow row per vector row, same order;
+* ``tombstones.i64``   — int64 global row ids deleted by later upserts (append-only);
+* ``manifest.json``    — ``{"dim", "segments": [{"name", "rows"}], "tombstones": n}``,
+                         replaced atomically (write + fsync + ``os.replace``) after the
+                         segment / tombstone bytes are durable, so a crash leaves either
+                         the old or the new table, never a torn one.
+
+Global row ids are the concatenation order of the segments, i.e. the GPU index's row ids,
+so a reopened table returns the same rows in the same tie order (score desc, row asc).
+Readers replay only the segments and tombstones the manifest lists.
+"""
+from __future__ import annotations
+
+import json
+import os
+from dataclasses import dataclass
+from typing import Any, Dict, Iterator, List, Optional, Sequence
+
+import numpy as np
+
+COLUMNS = ("chunk_id", "user_id", "document_id", "modality", "meta")
+
+
+def _fsync_write(path: str, data: bytes) -> None:
+    tmp = path + ".tmp"
+    with open(tmp, "wb") as f:
+        f.write(data)
+        f.flush()
+        os.fsync(f.fileno())
+    os.replace(tmp, path)
+
+
+@dataclass
+class Segment:
+    vectors: np.ndarray          # f32 [n, dim] (memory-mapped)
+    rows: Dict[str, List[Any]]   # column -> values
+
+
+class CorpusFiles:
+    """Append-only segment files of one table."""
+
+    def __init__(self, directory: str):
+        self.dir = directory
+        self.manifest_path = os.path.join(directory, "manifest.json")
+        self.manifest: Dict[str, Any] = {"dim": None, "segments": [], "tombstones": 0}
+        if os.path.exists(self.manifest_path):
+            with open(self.manifest_path) as f:
+                self.manifest = json.load(f)
+
+    @property
+    def dim(self) -> Optional[int]:
+        return self.manifest["dim"]
+
+    @property
+    def num_rows(self) -> int:
+        return sum(s["rows"] for s in self.manifest["segments"])
+
+    def append(self, vectors: np.ndarray, rows: Sequence[Dict[str, Any]], dead: Sequence[int] = ()) -> None:
+        """Durably append one upsert: its tombstones (row ids it replaces) and its rows."""
+        import pyarrow as pa
+        import pyarrow.parquet as pq
+
+        v = np.ascontiguousarray(vectors, dtype="<f4")
+        if v.ndim != 2 or v.shape[0] != len(rows):
+            raise ValueError("vectors must be [n, dim] with one payload row each")
+        m = json.loads(json.dumps(self.manifest))  # committed to self.manifest only on success
+        if m["dim"] is None:
+            m["dim"] = int(v.shape[1])
+        elif v.shape[1] != m["dim"]:
+            raise ValueError(f"dim {v.shape[1]} != table dim {m['dim']}")
+        os.makedirs(self.dir, exist_ok=True)
+        if len(dead):
+            path = os.path.join(self.dir, "tombstones.i64")
+            with open(path, "ab"):
+                pass
+            with open(path, "r+b") as f:
+                f.truncate(m["tombstones"] * 8)  # drop bytes of an uncommitted append
+                f.seek(0, os.SEEK_END)
+                f.write(np.asarray(dead, dtype="<i8").tobytes())
+                f.flush()
+                os.fsync(f.fileno())
+            m["tombstones"] += len(dead)
+        if v.shape[0]:
+            name = f"seg_{len(m['segments']):06d}"
+            _fsync_write(os.path.join(self.dir, name + ".f32"), v.tobytes())
+            table = pa.table({c: [str(r[c]) for r in rows] for c in COLUMNS})
+            tmp = os.path.join(self.dir, name + ".parquet.tmp")
+            pq.write_table(table, tmp)
+            with open(tmp, "rb") as f:
+                os.fsync(f.fileno())
+            os.replace(tmp, os.path.join(self.dir, name + ".parquet"))
+            m["segments"].append({"name": name, "rows": int(v.shape[0])})
+        _fsync_write(self.manifest_path, json.dumps(m).encode())
+        self.manifest = m
+
+    def segments(self) -> Iterator[Segment]:
+        import pyarrow.parquet as pq
+
+        dim = self.manifest["dim"]
+        for s in self.manifest["segments"]:
+            vec = np.memmap(os.path.join(self.dir, s["name"] + ".f32"), dtype="<f4", mode="r",
+                            shape=(s["rows"], dim))
+            t = pq.read_table(os.path.join(self.dir, s["name"] + ".parquet")).to_pydict()
+            yield Segment(vectors=vec, rows=t)
+
+    def tombstones(self) -> np.ndarray:
+        n = self.manifest["tombstones"]
+        if n == 0:
+            return np.empty(0, dtype=np.int64)
+        return np.fromfile(os.path.join(self.dir, "tombstones.i64"), dtype="<i8", count=n).astype(np.int64)
+
+
+__all__ = ["CorpusFiles", "Segment", "COLUMNS"]

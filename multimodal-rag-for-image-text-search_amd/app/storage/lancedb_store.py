@@ -10,6 +10,9 @@ become ``app.vector_store.FlatIndex`` objects resident in HBM; the ``user_id`` f
 becomes an int32 row label (prefilter); a per-row delete becomes a tombstone label.
 Every ``LanceDBStore`` opened on the same directory shares the same tables (the
 reference's two handles on one directory could miss each other's writes).
+Tables persist under ``<db_path>/mrag_tables/<table>/`` (``app.storage.corpus_files``:
+fp32 row segments + Parquet payloads + tombstones, atomic manifest) and are replayed into
+the GPU index on first use in a new process, with the same row ids.
 Semantics pinned in DESIGN.md §3: exact flat cosine (no IVF_PQ — the reference's
 index build is attempted on an empty table and swallowed, :51-60), prefilter, order
 (score desc, row asc), ``limit(max(top_k, 1))``, ``score = 1 - f32(1 - cos)``.
@@ -38,11 +41,17 @@ class VectorRow:
 
 
 class _Table:
-    """One collection: GPU rows + host-side row payloads."""
+    """One collection: GPU rows + host-side row payloads (+ their files, if persistent)."""
 
-    def __init__(self, name: str, device: int = 0):
+    def __init__(self, name: str, device: int = 0, directory: Optional[str] = None):
         self.name = name
         self.device = device
+        self.files = None
+        if directory is not None:
+            from app.storage.corpus_files import CorpusFiles
+
+            self.files = CorpusFiles(directory)
+        self._loaded = self.files is None or self.files.num_rows == 0
         self.index = None  # FlatIndex, created on the first write (dim unknown before)
         self.dim: Optional[int] = None
         self.chunk_ids: List[str] = []
@@ -61,10 +70,36 @@ class _Table:
         elif dim != self.dim:
             raise ValueError(f"{self.name}: embedding dim {dim} != table dim {self.dim}")
 
+    def _load(self) -> None:
+        """Replay the table's segments + tombstones into the GPU index (once per process)."""
+        if self._loaded:
+            return
+        self._loaded = True
+        self._ensure_index(self.files.dim)
+        for seg in self.files.segments():
+            cols = seg.rows
+            labs = np.asarray([self.labels.setdefault(u, len(self.labels)) for u in cols["user_id"]], dtype=np.int32)
+            first = self.index.add(np.asarray(seg.vectors), labs)
+            for i, cid in enumerate(cols["chunk_id"]):
+                self.chunk_ids.append(cid)
+                self.metas.append(cols["meta"][i])
+                self.doc_ids.append(cols["document_id"][i])
+                self.by_chunk.setdefault(cid, []).append(first + i)
+        dead = self.files.tombstones()
+        if dead.size:
+            self.index.delete(dead)
+            for r in dead.tolist():
+                rows = self.by_chunk.get(self.chunk_ids[r])
+                if rows and r in rows:
+                    rows.remove(r)
+                    if not rows:
+                        del self.by_chunk[self.chunk_ids[r]]
+
     def upsert(self, payloads: List[Dict[str, Any]]) -> None:
         if not payloads:
             return
         with self.lock:
+            self._load()
             emb = np.asarray([p["embedding"] for p in payloads], dtype=np.float32)
             if emb.ndim != 2:
                 raise ValueError("all embeddings in one upsert must have the same length")
@@ -73,6 +108,13 @@ class _Table:
             dead = []
             for p in payloads:
                 dead.extend(self.by_chunk.pop(p["chunk_id"], []))
+            if self.files is not None:  # durable first: a failed write leaves the table as it was
+                try:
+                    self.files.append(emb, payloads, dead)
+                except Exception:
+                    for r in dead:
+                        self.by_chunk.setdefault(self.chunk_ids[r], []).append(r)
+                    raise
             if dead:
                 self.index.delete(dead)
             labs = np.asarray([self.labels.setdefault(p["user_id"], len(self.labels)) for p in payloads],
@@ -86,6 +128,7 @@ class _Table:
 
     def search(self, user_id: str, vector: List[float], k: int) -> List[Dict[str, Any]]:
         with self.lock:
+            self._load()
             label = self.labels.get(user_id)
             if self.index is None or label is None:
                 return []
@@ -114,7 +157,9 @@ def _tables_for(db_path: str) -> Dict[str, _Table]:
     with _REG_LOCK:
         if key not in _REGISTRY:
             dev = int(os.environ.get("MRAG_DEVICE", "0"))
-            _REGISTRY[key] = {n: _Table(n, dev) for n in ("text_collection", "image_collection")}
+            persist = os.environ.get("MRAG_STORE_PERSIST", "1") != "0"
+            _REGISTRY[key] = {n: _Table(n, dev, os.path.join(key, "mrag_tables", n) if persist else None)
+                              for n in ("text_collection", "image_collection")}
         return _REGISTRY[key]
 
 

@@ -136,3 +136,30 @@ def test_index_retrieve_end_to_end(cuda, tmp_path, monkeypatch):
     for a, b in zip(single, batched):
         assert [x["chunk_id"] for x in a] == [x["chunk_id"] for x in b]
         assert [x["combined_score"] for x in a] == pytest.approx([x["combined_score"] for x in b], abs=1e-5)
+
+
+def test_store_persists_across_restart(cuda, tmp_path):
+    """LanceDBStore tables survive a new process (registry dropped): same rows, same ids,
+    same tie order; re-upserts (delete + add) and per-user filtering replayed."""
+    from app.storage import lancedb_store as ls
+
+    db = str(tmp_path / "persist")
+    rng = np.random.default_rng(9)
+    vecs = rng.standard_normal((300, 64)).astype(np.float32)
+    vecs[7] = vecs[3]  # an exact tie
+    store = ls.LanceDBStore(db)
+    store.upsert_text_vectors([ls.VectorRow(f"c{i}", "u1" if i % 3 else "u2", f"d{i}", "text", vecs[i], {"i": i})
+                               for i in range(300)])
+    store.upsert_text_vectors([ls.VectorRow("c5", "u1", "d5", "text", vecs[100], {"i": "new"})])  # replaces c5
+    queries = rng.standard_normal((4, 64)).astype(np.float32)
+    queries[0] = vecs[3]
+    before = [(store.search_text(u, q, 12)) for q in queries for u in ("u1", "u2")]
+    ls._REGISTRY.clear()  # what a new process sees
+    again = ls.LanceDBStore(db)
+    after = [(again.search_text(u, q, 12)) for q in queries for u in ("u1", "u2")]
+    assert before == after
+    hits = again.search_text("u1", vecs[100], 5)  # c5 was re-upserted with c100's vector
+    ids = [h["chunk_id"] for h in hits]
+    assert ids[:2] == ["c100", "c5"]  # exact tie: older row first
+    assert [h["meta"] for h in hits[:2]] == [{"i": 100}, {"i": "new"}]
+    assert again.search_text("u1", vecs[5], 1)[0]["chunk_id"] != "c5"  # the replaced row stays deleted
