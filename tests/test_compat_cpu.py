@@ -302,3 +302,36 @@ def test_tokenizers_fallback():
         ClipTokenizer()([" ".join(["word"] * 100)])
     long_ids, _ = WordPieceTokenizer()([" ".join(["word"] * 400)])
     assert long_ids.shape[1] == 256
+
+
+def test_splitter_algorithm_properties():
+    """llama_index SentenceSplitter restatement (§8f row 4; unpinned without tiktoken/nltk):
+    with a pluggable whitespace tokenizer every chunk fits the (metadata-aware) budget,
+    chunks cover the text in order, each chunk after the first opens with at most
+    chunk_overlap tokens of its predecessor's tail, and an over-long unpunctuated run is
+    split down to words."""
+    from app.ml.splitter import Document, SentenceSplitter
+
+    tok = str.split
+    sp = SentenceSplitter(chunk_size=12, chunk_overlap=4, tokenizer=tok)
+    rng = np.random.default_rng(0)
+    sents = [" ".join(f"w{j}" for j in rng.integers(0, 99, int(rng.integers(2, 9)))) + "." for _ in range(40)]
+    text = " ".join(sents[:20]) + "\n\n\n" + " ".join(sents[20:]) + " " + " ".join(f"x{i}" for i in range(30))
+    chunks = sp.split_text(text)
+    assert all(len(tok(c)) <= 12 for c in chunks)
+    words = tok(text)
+    pos = 0
+    for i, c in enumerate(chunks):  # each chunk = overlap (<= 4 tokens) + new words, in order
+        cw = tok(c)
+        start = words.index(cw[0], max(0, pos - 4))
+        assert words[start:start + len(cw)] == cw
+        assert pos - start <= 4
+        pos = start + len(cw)
+    assert pos == len(words)
+    meta = {"source": "pdf", "page_no": 3}
+    nodes = sp.get_nodes_from_documents([Document(text=text, metadata=meta, doc_id="d")])
+    budget = 12 - len(tok("source: pdf\npage_no: 3"))
+    # a new chunk always takes its first split on top of the carried overlap (<= 4 tokens)
+    assert all(len(tok(n.text)) <= budget + 4 for n in nodes) and max(len(tok(n.text)) for n in nodes) > budget
+    with pytest.raises(ValueError):
+        sp.split_text_metadata_aware("a b c", "k: " + " ".join(["v"] * 20))
