@@ -265,7 +265,9 @@ __global__ __launch_bounds__(SCAN_THREADS) void knn_scan_kernel(ScanParams p) {
       const float s = row_ok(lane_mask, blk, reg) ? acc[reg] : -INFINITY;
       const int row = tile * TILE_ROWS + blk * 32 + 8 * (reg >> 2) + 4 * h + (reg & 3);
       if constexpr (COLLECT) {
-        if (s >= thr_collect) {
+        // row_ok explicitly: masked rows carry -inf, which a -inf threshold (fewer than
+        // k candidates in K8) would otherwise accept — padding and other users' rows
+        if (row_ok(lane_mask, blk, reg) && s >= thr_collect) {
           const int pos = atomicAdd(p.cand_cnt + slot, 1);
           if (pos < p.ccap) p.cand[(size_t)slot * p.ccap + pos] = row;
         }

@@ -209,3 +209,25 @@ def test_seeded_threshold_prepass(cuda, label_filter):
         s, r = ix.search(q, k, label=label_filter)
         os_, or_ = flat_cosine_topk(x, lab, q, k, label_filter=label_filter)
         _check(s, r, os_, or_)
+
+
+@pytest.mark.parametrize("dim", [384, 512])
+def test_small_tables_k_above_list_depth(cuda, dim):
+    """Tables of a few tiles with k above the per-split list depth (the reference's
+    per-user tables at k = 50 / 12): K8 cannot certify, the collect pass runs with a
+    -inf threshold and must still honour the label prefilter and skip padding rows."""
+    from app.vector_store import FlatIndex
+
+    for n in (1, 15, 40, 64, 65, 130):
+        for k in (10, 33, 50, 100):
+            rng = np.random.default_rng(n * 7 + k)
+            x = rng.standard_normal((n, dim)).astype(np.float32)
+            lab = rng.integers(0, 2, n).astype(np.int32)
+            q = rng.standard_normal((3, dim)).astype(np.float32)
+            ix = FlatIndex(dim)
+            ix.add(x, lab)
+            for f in (-1, 0, 1, 2):
+                s, r = ix.search(q, k, label=f)
+                os_, or_ = flat_cosine_topk(x, lab, q, k, label_filter=f)
+                _check(s, r, os_, or_)
+            ix.close()
