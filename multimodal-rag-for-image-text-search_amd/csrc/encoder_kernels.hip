@@ -31,27 +31,46 @@ __device__ __forceinline__ void glds_x4(const void* gsrc, uint32_t lds_addr) {
 
 // ---------------------------------------------------------------------------
 // K3: C[m][n] (+)= act(sum_k A[m][k] W[n][k] + bias[n])   (the "NT" GEMM of nn.Linear)
-// 128x128x64 block tile, 4 waves (2x2) of 64x64, MFMA 32x32x16 f16 -> f32.
-// Operands staged to LDS by LDS-DMA, 128-byte rows with chunk c stored at position
-// c ^ ((row >> 1) & 7) (source-address swizzle) so every ds_read_b128 fragment read is
-// bank-conflict free; 2 stages, one barrier per 64-deep k-step.
+//
+// Both GEMM kernels use MFMA 16x16x32 f16 with the WEIGHT fragment as the MFMA's A operand
+// and the activation fragment as its B operand, i.e. they compute C^T blocks: lane l holds
+// output row m = (l & 15) and the four consecutive columns n = 4 (l >> 4) + r, r = 0..3,
+// so the epilogue stores 8 B (f16) or 16 B (f32) per lane instead of one element.
+// Operands are staged to LDS by LDS-DMA into 128-byte rows (64 k of one row) with 16-byte
+// chunk c stored at position c ^ ((row >> 1) & 7) (source-address swizzle): every
+// ds_read_b128 fragment read of 16 consecutive rows is bank-conflict free.
+// Every output element is accumulated in the same order by both kernels (32-deep MFMA
+// chunks in ascending k, one accumulator) and finished by the same gemm_store4, so a row's
+// result does not depend on which kernel its batch size selected.
 template <int EPI>
-__device__ __forceinline__ void gemm_store(const GemmArgs& g, int m, int n, float v) {
+__device__ __forceinline__ void gemm_store4(const GemmArgs& g, int m, int n, f32x4 v, const float* bn) {
+#pragma unroll
+  for (int r = 0; r < 4; ++r) v[r] += bn[r];
   const size_t o = (size_t)m * g.ldc + n;
-  if constexpr (EPI == EPI_F16) {
-    ((_Float16*)g.C)[o] = (_Float16)v;
-  } else if constexpr (EPI == EPI_F16_QUICK_GELU) {
-    // x * sigmoid(1.702 x) with hardware exp2 / rcp (~1 ulp each; the result is rounded
-    // to fp16) instead of a full-precision divide
-    v = v * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.702f * 1.44269504088896341f * v));
-    ((_Float16*)g.C)[o] = (_Float16)v;
-  } else if constexpr (EPI == EPI_F16_GELU_ERF) {
-    v = 0.5f * v * (1.0f + erff(v * 0.70710678118654752f));
-    ((_Float16*)g.C)[o] = (_Float16)v;
+  if constexpr (EPI == EPI_F16 || EPI == EPI_F16_QUICK_GELU || EPI == EPI_F16_GELU_ERF) {
+    typedef _Float16 half4 __attribute__((ext_vector_type(4)));
+    half4 h;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float x = v[r];
+      if constexpr (EPI == EPI_F16_QUICK_GELU) {
+        // x * sigmoid(1.702 x) with hardware exp2 / rcp (~1 ulp each; the result is
+        // rounded to fp16) instead of a full-precision divide
+        x = x * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.702f * 1.44269504088896341f * x));
+      } else if constexpr (EPI == EPI_F16_GELU_ERF) {
+        x = 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));
+      }
+      h[r] = (_Float16)x;
+    }
+    *(half4*)((_Float16*)g.C + o) = h;
   } else if constexpr (EPI == EPI_F32_RESIDUAL) {
-    ((float*)g.C)[o] += v;
+    f32x4* p = (f32x4*)((float*)g.C + o);
+    f32x4 c = *p;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) c[r] += v[r];
+    *p = c;
   } else {
-    ((float*)g.C)[o] = v;
+    *(f32x4*)((float*)g.C + o) = v;
   }
 }
 
@@ -61,17 +80,22 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
 }
 
+// fragment offset (bytes) of row j, 16-byte chunk c, in a swizzled 128-byte-row LDS image
+__device__ __forceinline__ int swz_off(int j, int c) { return j * 128 + ((c ^ ((j >> 1) & 7)) * 16); }
+
 constexpr int GM = 128, GN = 128, GK = 64;
 constexpr int GTHREADS = 256;
 constexpr int STAGE_BYTES = (GM + GN) * GK * 2;  // 32 KiB
 
+// K3 (small M: text queries, short batches, N not a multiple of 256): 128 x 128 x 64 block
+// tile, 4 waves (2 x 2) of 64 x 64, 2 stages, one barrier per k-step; 2 workgroups per CU.
 template <int EPI>
 __global__ __launch_bounds__(GTHREADS) void gemm_nt_kernel(GemmArgs g) {
   __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_BYTES];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wr = w >> 1, wc = w & 1;
-  const int h = lane >> 5, r32 = lane & 31;
+  const int fr = lane & 15, fq = lane >> 4;
   const uint32_t lds_base = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)((AS3 char*)smem));
 
   const int tiles_n = g.N / GN;
@@ -98,186 +122,256 @@ __global__ __launch_bounds__(GTHREADS) void gemm_nt_kernel(GemmArgs g) {
     }
   };
 
-  f32x16 acc[2][2];
+  f32x4 acc[4][4];  // [activation block i][weight block jb]
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{};
 
-  const int sw = (r32 >> 1) & 7;
+  int offA[4][2], offW[4][2];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      offA[i][kk] = swz_off(wr * 64 + 16 * i + fr, kk * 4 + fq);
+      offW[i][kk] = GM * GK * 2 + swz_off(wc * 64 + 16 * i + fr, kk * 4 + fq);
+    }
+
   stage(0, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   for (int ks = 0; ks < ksteps; ++ks) {
     const int cur = ks & 1;
     if (ks + 1 < ksteps) stage(cur ^ 1, (ks + 1) * GK);
-    const char* At = (const char*)smem + cur * STAGE_BYTES;
-    const char* Bt = At + GM * GK * 2;
-    // read all 16 fragments of this 64-deep step first (64 VGPRs), then 16 MFMAs: the LDS
-    // latency of later sub-steps hides under the earlier MFMAs
-    half8 a[GK / 16][2], b[GK / 16][2];
+    const char* st = (const char*)smem + cur * STAGE_BYTES;
+    half8 a[4][2], b[4][2];
 #pragma unroll
-    for (int kk = 0; kk < GK / 16; ++kk) {
-      const int coff = (((2 * kk + h) ^ sw) * 16);
+    for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-      for (int i = 0; i < 2; ++i) a[kk][i] = *(const half8*)(At + (wr * 64 + i * 32 + r32) * 128 + coff);
+      for (int i = 0; i < 4; ++i) {
+        a[i][kk] = *(const half8*)(st + offA[i][kk]);
+        b[i][kk] = *(const half8*)(st + offW[i][kk]);
+      }
 #pragma unroll
-      for (int j = 0; j < 2; ++j) b[kk][j] = *(const half8*)(Bt + (wc * 64 + j * 32 + r32) * 128 + coff);
-    }
-    __builtin_amdgcn_sched_barrier(0);  // keep the reads ahead (hipcc would re-interleave them)
+    for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-    for (int kk = 0; kk < GK / 16; ++kk)
+      for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[kk][i], b[kk][j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[j][kk], a[i][kk], acc[i][j], 0, 0, 0);
     __builtin_amdgcn_sched_barrier(0);  // MFMAs stay ahead of the stage wait + barrier
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
 
-  // epilogue: lane owns column n of each 32x32 block and rows (reg&3)+8(reg>>2)+4h
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int n = n0 + wc * 64 + j * 32 + r32;
-    const float bn = g.bias ? g.bias[n] : 0.f;
+  for (int j = 0; j < 4; ++j) {
+    const int n = n0 + wc * 64 + 16 * j + 4 * fq;
+    float bn[4];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int r = 0; r < 4; ++r) bn[r] = g.bias ? g.bias[n + r] : 0.f;
 #pragma unroll
-      for (int reg = 0; reg < 16; ++reg) {
-        const int m = m0 + wr * 64 + i * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
-        // one epilogue for every GEMM kernel: a row's result must not depend on which
-        // kernel the batch size selected
-        if (m < g.M) gemm_store<EPI>(g, m, n, acc[i][j][reg] + bn);
-      }
+    for (int i = 0; i < 4; ++i) {
+      const int m = m0 + wr * 64 + 16 * i + fr;
+      if (m < g.M) gemm_store4<EPI>(g, m, n, acc[i][j], bn);
     }
   }
 }
 
 // ---------------------------------------------------------------------------
-// K3b: the same GEMM for the big-M encoder batches (M >= 1024 rows: ViT at batch 256 is
-// M = 12,800), 256 x BN block tile, 8 waves as 2 (M) x 4 (N) of 128 x BN/4, BK = 64.
-// One workgroup per CU (128 KiB LDS at BN = 256): each A fragment read from LDS feeds
-// BN/128 MFMAs and each B fragment four, half the LDS bytes per MFMA of K3.
-// Pipeline per 64-deep k-step: the next k-step's tile is staged by LDS-DMA in pieces
-// spread over the four 16-deep sub-steps (one job per MFMA cluster), the fragments of
-// sub-step kk+1 are read while the MFMAs of kk run (two register sets), and one
-// vmcnt(0) + barrier closes the k-step. Block ids are remapped so that the blocks of one
-// A panel (same tm) run on the same XCD (bijective for any grid size).
-constexpr int GB_BM = 256, GB_THREADS = 512;
+// K3d (M >= 1024, N % 256 == 0: the ViT batches): 256 x 256 x 64 tiles, 8 waves (2 M x 4 N,
+// 128 x 64 each), an eight-phase pipeline whose LDS-DMA prefetch stays in flight across
+// barriers, and two wave groups in ping-pong.
+//
+// A K-tile is staged as four 16 KiB half-tiles ("slots"), each 128 LDS rows x 128 B:
+//   slot 0 A-h0: tile rows {0..63, 128..191}   slot 1 B-h0: tile cols {64w + 0..31}
+//   slot 2 B-h1: tile cols {64w + 32..63}      slot 3 A-h1: tile rows {64..127, 192..255}
+// (A = activations, B = weights) so that each of the four phases of a K-tile computes one
+// 64 x 32 quadrant of every wave's 128 x 64 output over the full BK = 64 and reads exactly
+// one new slot (phase 0 also B-h0): A-h0 + B-h0 -> (h0, hh0); B-h1 -> (h0, hh1); A-h1 ->
+// (h1, hh1); nothing -> (h1, hh0). A slot is dead after its only read phase and is restaged
+// one phase later with the K-tile two ahead (two LDS buffers x four slots = 128 KiB).
+// Load sequence L[i] = slot (i & 3) of K-tile i >> 2; phase phi = 4t + p issues L[phi + 7]
+// (the prologue issues L[0..6]) and waits until L[phi + 2] has landed — what phase phi + 1
+// reads — leaving the five younger half-tiles (10 LDS-DMA instructions per wave) in flight:
+// one counted `s_waitcnt vmcnt`, never 0 in the loop.
+// Phase: ds_reads -> issue -> vmcnt(N) + lgkmcnt(0) -> s_barrier -> MFMAs (setprio 1) ->
+// s_barrier, with the two wave groups one barrier apart (ping-pong: on every SIMD one
+// wave's MFMA segment overlaps the other wave's read segment). A wave's reads of phase phi
+// are retired before the barrier that ends its read segment, which every wave passes before
+// issuing phase phi + 1's LDS-DMA (WAR: a slot may be restaged one phase after its read);
+// the vmcnt waits of phase phi precede the barrier ending the later group's read segment,
+// which precedes every read of phase phi + 1 (RAW).
+constexpr int G8_BM = 256, G8_BN = 256, G8_THREADS = 512;
+constexpr int G8_SLOT = 16384;
 
-template <int BN, int EPI, bool EARLY = true>
-__global__ __launch_bounds__(GB_THREADS) void gemm_big_kernel(GemmArgs g) {
-  constexpr int WN = BN / 4;                   // wave tile 128 x WN
-  constexpr int TM = 4, TN = WN / 32;          // 32x32 blocks per wave
-  constexpr int A_BYTES = GB_BM * GK * 2;      // 32 KiB
-  constexpr int STAGE = (GB_BM + BN) * GK * 2;
-  constexpr int PIECES = (GB_BM + BN) / 8;     // 1 KiB = 8 rows x 128 B
-  constexpr int PPW = PIECES / 8;              // per wave per k-step
-  static_assert(PIECES % 8 == 0 && PPW <= 8, "pieces per wave");
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+__device__ __forceinline__ void g8_wait_vm(int younger_halves) {
+  switch (younger_halves) {  // wave-uniform: 2 LDS-DMA instructions per half-tile
+    case 5: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
+}
+
+// ABL (timing experiments only, wrong results): 1 = no LDS-DMA in the loop, 2 = no
+// fragment ds_reads in the loop, 3 = both, 4 = no ping-pong stagger
+template <int EPI, int ABL = 0>
+__global__ __launch_bounds__(G8_THREADS) void gemm_8p_kernel(GemmArgs g) {
+  __shared__ __attribute__((aligned(16))) char smem[8 * G8_SLOT];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wr = w >> 2, wc = w & 3;
-  const int h = lane >> 5, r32 = lane & 31;
+  const int fr = lane & 15, fq = lane >> 4;
   const uint32_t lds_base = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)((AS3 char*)smem));
 
-  const int tiles_n = g.N / BN;
-  const int nwg = gridDim.x;
-  const int t = xcd_remap(blockIdx.x, nwg);
+  const int tiles_n = g.N / G8_BN;
+  const int t = xcd_remap(blockIdx.x, gridDim.x);
   const int tm = t / tiles_n, tn = t - (t / tiles_n) * tiles_n;
-  const int m0 = tm * GB_BM, n0 = tn * BN;
-  const int ksteps = g.K / GK;
+  const int m0 = tm * G8_BM, n0 = tn * G8_BN;
+  const int total = (g.K / GK) * 4;  // half-tiles
 
-  // piece P of a stage: rows 8(P mod ...) .. +8 of A (P < 32) or of W; lane -> row rr, chunk pos
-  auto stage_piece = [&](int buf, int k0, int i) {
-    const int P = w * PPW + i;
-    const int rr = lane >> 3, pos = lane & 7;
-    const _Float16* src;
-    int row;
-    if (P < GB_BM / 8) {
-      row = 8 * P + rr;
-      const int c = pos ^ ((row >> 1) & 7);
-      src = g.A + (size_t)min(m0 + row, g.M - 1) * g.lda + k0 + c * 8;
-    } else {
-      row = 8 * (P - GB_BM / 8) + rr;
-      const int c = pos ^ ((row >> 1) & 7);
-      src = g.W + (size_t)(n0 + row) * g.ldw + k0 + c * 8;
+  // staging: this wave fills pieces 2w, 2w + 1 (8 LDS rows each) of every slot; LDS row
+  // j = 16 w + 8 q + (lane >> 3), chunk position lane & 7 holds source chunk
+  // (lane & 7) ^ ((j >> 1) & 7)
+  const _Float16* srcA[2][2];
+  const _Float16* srcB[2][2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int j = 16 * w + 8 * q + (lane >> 3);
+    const int c = (lane & 7) ^ ((j >> 1) & 7);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int row = (j & 63) + 128 * (j >> 6) + 64 * h;
+      srcA[h][q] = g.A + (size_t)min(m0 + row, g.M - 1) * g.lda + c * 8;
+      const int col = 64 * (j >> 5) + 32 * h + (j & 31);
+      srcB[h][q] = g.W + (size_t)(n0 + col) * g.ldw + c * 8;
     }
-    glds_x4(src, lds_base + buf * STAGE + P * 1024);
+  }
+  auto stage = [&](int i) {  // L[i]: slot i & 3 of K-tile i >> 2
+    const int kt = i >> 2, sl = i & 3;
+    const int k0 = kt * GK;
+    const uint32_t dst = lds_base + (uint32_t)(((kt & 1) * 4 + sl) * G8_SLOT) + (uint32_t)(w * 2048);
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const _Float16* src = (sl == 0) ? srcA[0][q] : (sl == 1) ? srcB[0][q] : (sl == 2) ? srcB[1][q] : srcA[1][q];
+      glds_x4(src + k0, dst + q * 1024);
+    }
   };
 
-  f32x16 acc[TM][TN];
+  int offA[4][2], offB[2][2];
 #pragma unroll
-  for (int i = 0; i < TM; ++i)
+  for (int kk = 0; kk < 2; ++kk) {
 #pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = f32x16{};
-
-  const int sw = (r32 >> 1) & 7;
-  // fragment offsets (bytes within a stage): A row wr*128 + 32i + r32, B row wc*WN + 32j + r32
-  const int offA = (wr * 128 + r32) * 128;
-  const int offB = A_BYTES + (wc * WN + r32) * 128;
-  half8 fa[2][TM], fb[2][TN];
-  auto read_frags = [&](int set, int buf, int kk) {
-    const char* st = (const char*)smem + buf * STAGE;
-    const int coff = ((2 * kk + h) ^ sw) * 16;
+    for (int i = 0; i < 4; ++i) offA[i][kk] = swz_off(64 * wr + 16 * i + fr, kk * 4 + fq);
 #pragma unroll
-    for (int i = 0; i < TM; ++i) fa[set][i] = *(const half8*)(st + offA + i * 32 * 128 + coff);
-#pragma unroll
-    for (int j = 0; j < TN; ++j) fb[set][j] = *(const half8*)(st + offB + j * 32 * 128 + coff);
-  };
-
-#pragma unroll
-  for (int i = 0; i < PPW; ++i) stage_piece(0, 0, i);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  for (int ks = 0; ks < ksteps; ++ks) {
-    const int cur = ks & 1;
-    const bool more = ks + 1 < ksteps;
-    read_frags(0, cur, 0);
-#pragma unroll
-    for (int kk = 0; kk < GK / 16; ++kk) {
-      const int set = kk & 1;
-      if (kk + 1 < GK / 16) read_frags(set ^ 1, cur, kk + 1);
-      // next k-step's pieces: all at the first sub-step (EARLY: a full k-step of latency
-      // cover before the closing vmcnt(0)), or spread over the four sub-steps
-      if constexpr (EARLY) {
-        if (kk == 0) {
-#pragma unroll
-          for (int i = 0; i < PPW; ++i)
-            if (more) stage_piece(cur ^ 1, (ks + 1) * GK, i);
-        }
-      } else {
-#pragma unroll
-        for (int i = kk * PPW / 4; i < (kk + 1) * PPW / 4; ++i)
-          if (more) stage_piece(cur ^ 1, (ks + 1) * GK, i);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[set][i], fb[set][j], acc[i][j], 0, 0, 0);
-      __builtin_amdgcn_s_setprio(0);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    for (int jb = 0; jb < 2; ++jb) offB[jb][kk] = swz_off(32 * wc + 16 * jb + fr, kk * 4 + fq);
   }
 
-  // epilogue: lane owns column n of each 32x32 block and rows (reg&3)+8(reg>>2)+4h
+  f32x4 acc[2][2][4][2];  // [h][hh][i][jb]
 #pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int n = n0 + wc * WN + j * 32 + r32;
-    const float bn = g.bias ? g.bias[n] : 0.f;
+  for (int h = 0; h < 2; ++h)
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
+    for (int hh = 0; hh < 2; ++hh)
 #pragma unroll
-      for (int reg = 0; reg < 16; ++reg) {
-        const int m = m0 + wr * 128 + i * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
-        if (m < g.M) gemm_store<EPI>(g, m, n, acc[i][j][reg] + bn);
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int jb = 0; jb < 2; ++jb) acc[h][hh][i][jb] = f32x4{};
+
+  half8 fa[4][2], fb0[2][2], fb1[2][2];
+  auto readA = [&](const char* slot) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        if constexpr (ABL == 2 || ABL == 3) asm volatile("" : "+v"(fa[i][kk]));
+        else fa[i][kk] = *(const half8*)(slot + offA[i][kk]);
+      }
+  };
+  auto readB = [&](const char* slot, half8 (&fb)[2][2]) {
+#pragma unroll
+    for (int jb = 0; jb < 2; ++jb)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        if constexpr (ABL == 2 || ABL == 3) asm volatile("" : "+v"(fb[jb][kk]));
+        else fb[jb][kk] = *(const half8*)(slot + offB[jb][kk]);
+      }
+  };
+  auto mfma_q = [&](f32x4 (&a)[4][2], const half8 (&fb)[2][2]) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int jb = 0; jb < 2; ++jb)
+          a[i][jb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fb[jb][kk], fa[i][kk], a[i][jb], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto bar = [&]() {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  // end of a read segment: issue L[phi + 7], wait for L[phi + 2] (read by phase phi + 1)
+  // and for this segment's own ds_reads, barrier
+  auto end_reads = [&](int phi) {
+    if (ABL != 1 && ABL != 3 && phi + 7 < total) stage(phi + 7);
+    g8_wait_vm(min(5, max(0, total - 1 - (phi + 2))));
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    bar();
+  };
+
+  {  // prologue: L[0..6], then L[0], L[1] landed
+    const int last = min(6, total - 1);
+    for (int i = 0; i <= last; ++i) stage(i);
+    g8_wait_vm(min(5, max(0, total - 2)));
+    bar();
+  }
+  // waves 4..7 (one per SIMD beside a wave of 0..3) run one barrier behind waves 0..3
+  if (ABL != 4 && wr == 1) bar();
+  const int ktiles = total >> 2;
+  for (int kt = 0; kt < ktiles; ++kt) {
+    const char* buf = (const char*)smem + (kt & 1) * 4 * G8_SLOT;
+    const int phi = 4 * kt;
+    readA(buf + 0 * G8_SLOT);  // phase 0: (h0, hh0)
+    readB(buf + 1 * G8_SLOT, fb0);
+    end_reads(phi);
+    mfma_q(acc[0][0], fb0);
+    bar();
+    readB(buf + 2 * G8_SLOT, fb1);  // phase 1: (h0, hh1)
+    end_reads(phi + 1);
+    mfma_q(acc[0][1], fb1);
+    bar();
+    readA(buf + 3 * G8_SLOT);  // phase 2: (h1, hh1)
+    end_reads(phi + 2);
+    mfma_q(acc[1][1], fb1);
+    bar();
+    end_reads(phi + 3);  // phase 3: (h1, hh0) from registers
+    mfma_q(acc[1][0], fb0);
+    bar();
+  }
+  if (ABL != 4 && wr == 0) bar();  // same barrier count for both groups
+
+  // epilogue: block (h, hh, i, jb): row 128 wr + 64 h + 16 i + fr, columns
+  // 64 wc + 32 hh + 16 jb + 4 fq + (0..3)
+#pragma unroll
+  for (int hh = 0; hh < 2; ++hh) {
+#pragma unroll
+    for (int jb = 0; jb < 2; ++jb) {
+      const int n = n0 + 64 * wc + 32 * hh + 16 * jb + 4 * fq;
+      float bn[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bn[r] = g.bias ? g.bias[n + r] : 0.f;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int m = m0 + 128 * wr + 64 * h + 16 * i + fr;
+          if (m < g.M) gemm_store4<EPI>(g, m, n, acc[h][hh][i][jb], bn);
+        }
       }
     }
   }
@@ -616,8 +710,8 @@ __global__ void mean_pool_kernel(const float* __restrict__ X, const int32_t* __r
 
 // ---------------------------------------------------------------------------
 // launchers
-// env MRAG_GEMM_BIG (A/B timing): default -1 = K3b (BN 256 when N % 256 == 0, else 128) from
-// M >= 1024; 0 = K3 only; 256 / 128 = K3b at that tile width; 2 = K3b with the LDS-DMA spread
+// env MRAG_GEMM_BIG (A/B timing): default -1 = K3d for M >= 1024 and N % 256 == 0, K3 otherwise;
+// 0 = K3 only. MRAG_GEMM_ABL: K3d ablation builds (timing only, EPI_F16).
 int gemm_big_mode() {
   static const int v = [] {
     const char* e = getenv("MRAG_GEMM_BIG");
@@ -626,15 +720,28 @@ int gemm_big_mode() {
   return v;
 }
 
-template <int BN, bool EARLY>
-int launch_gemm_big(const GemmArgs& g, int epi, hipStream_t s) {
-  const dim3 grid((unsigned)(((g.M + GB_BM - 1) / GB_BM) * (g.N / BN)));
+int launch_gemm_8p(const GemmArgs& g, int epi, hipStream_t s) {
+  const dim3 grid((unsigned)(((g.M + G8_BM - 1) / G8_BM) * (g.N / G8_BN)));
+  static const int abl = [] {
+    const char* e = getenv("MRAG_GEMM_ABL");
+    return e ? atoi(e) : 0;
+  }();
+  if (abl != 0 && epi == EPI_F16) {
+    switch (abl) {
+      case 1: hipLaunchKernelGGL((gemm_8p_kernel<EPI_F16, 1>), grid, dim3(G8_THREADS), 0, s, g); break;
+      case 2: hipLaunchKernelGGL((gemm_8p_kernel<EPI_F16, 2>), grid, dim3(G8_THREADS), 0, s, g); break;
+      case 3: hipLaunchKernelGGL((gemm_8p_kernel<EPI_F16, 3>), grid, dim3(G8_THREADS), 0, s, g); break;
+      default: hipLaunchKernelGGL((gemm_8p_kernel<EPI_F16, 4>), grid, dim3(G8_THREADS), 0, s, g); break;
+    }
+    MRAG_CHECK_LAUNCH();
+    return MRAG_OK;
+  }
   switch (epi) {
-    case EPI_F16: hipLaunchKernelGGL((gemm_big_kernel<BN, EPI_F16, EARLY>), grid, dim3(GB_THREADS), 0, s, g); break;
-    case EPI_F16_QUICK_GELU: hipLaunchKernelGGL((gemm_big_kernel<BN, EPI_F16_QUICK_GELU, EARLY>), grid, dim3(GB_THREADS), 0, s, g); break;
-    case EPI_F16_GELU_ERF: hipLaunchKernelGGL((gemm_big_kernel<BN, EPI_F16_GELU_ERF, EARLY>), grid, dim3(GB_THREADS), 0, s, g); break;
-    case EPI_F32_RESIDUAL: hipLaunchKernelGGL((gemm_big_kernel<BN, EPI_F32_RESIDUAL, EARLY>), grid, dim3(GB_THREADS), 0, s, g); break;
-    case EPI_F32: hipLaunchKernelGGL((gemm_big_kernel<BN, EPI_F32, EARLY>), grid, dim3(GB_THREADS), 0, s, g); break;
+    case EPI_F16: hipLaunchKernelGGL(gemm_8p_kernel<EPI_F16>, grid, dim3(G8_THREADS), 0, s, g); break;
+    case EPI_F16_QUICK_GELU: hipLaunchKernelGGL(gemm_8p_kernel<EPI_F16_QUICK_GELU>, grid, dim3(G8_THREADS), 0, s, g); break;
+    case EPI_F16_GELU_ERF: hipLaunchKernelGGL(gemm_8p_kernel<EPI_F16_GELU_ERF>, grid, dim3(G8_THREADS), 0, s, g); break;
+    case EPI_F32_RESIDUAL: hipLaunchKernelGGL(gemm_8p_kernel<EPI_F32_RESIDUAL>, grid, dim3(G8_THREADS), 0, s, g); break;
+    case EPI_F32: hipLaunchKernelGGL(gemm_8p_kernel<EPI_F32>, grid, dim3(G8_THREADS), 0, s, g); break;
     default: return mrag::fail(MRAG_ERR_ARG, "gemm: bad epilogue %d", epi);
   }
   MRAG_CHECK_LAUNCH();
@@ -645,13 +752,8 @@ int launch_gemm(const GemmArgs& g, int epi, hipStream_t s) {
   if (g.M <= 0) return MRAG_OK;
   MRAG_REQUIRE(g.N % GN == 0 && g.K % GK == 0, "gemm: N=%d must be a multiple of %d and K=%d of %d", g.N, GN, g.K,
                GK);
-  MRAG_REQUIRE(g.lda % 8 == 0 && g.ldw % 8 == 0, "gemm: lda/ldw must be multiples of 8");
-  const int big = gemm_big_mode();
-  if (g.M >= 1024 && big != 0) {
-    if (big == 2) return g.N % 256 == 0 ? launch_gemm_big<256, false>(g, epi, s) : launch_gemm_big<128, false>(g, epi, s);
-    if ((big == -1 || big == 256) && g.N % 256 == 0) return launch_gemm_big<256, true>(g, epi, s);
-    if (big != 256) return launch_gemm_big<128, true>(g, epi, s);  // N % 128 == 0 (checked above)
-  }
+  MRAG_REQUIRE(g.lda % 8 == 0 && g.ldw % 8 == 0 && g.ldc % 4 == 0, "gemm: lda/ldw must be multiples of 8, ldc of 4");
+  if (gemm_big_mode() != 0 && g.M >= 1024 && g.N % G8_BN == 0) return launch_gemm_8p(g, epi, s);
   const dim3 grid((unsigned)(((g.M + GM - 1) / GM) * (g.N / GN)));
   switch (epi) {
     case EPI_F16: hipLaunchKernelGGL(gemm_nt_kernel<EPI_F16>, grid, dim3(GTHREADS), 0, s, g); break;

@@ -41,6 +41,10 @@ def run(name, reps=20):
     torch.cuda.synchronize()
     us = e0.elapsed_time(e1) * 1e3 / reps
     out = {"shape": name, "M": M, "N": N, "K": K, "us": round(us, 1), "TFLOPs": round(2 * M * N * K / us / 1e6, 1)}
+    if epi == 0:  # numerics vs a torch fp32 product of the same fp16 operands
+        gemm_nt(A, W, bias, C, epi)
+        ref = A.float() @ W.float().t()
+        out["rel_err"] = float((C.float() - ref).abs().max() / ref.abs().max())
     if os.environ.get("TORCH_REF") == "1":  # vendor library on the same shape (reference point only)
         Wt = W.t()
         for _ in range(5):
