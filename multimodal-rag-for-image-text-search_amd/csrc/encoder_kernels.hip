@@ -11,6 +11,7 @@
 // input is f16 (LayerNorm writes the f16 copy), weights are f16 [out][in] (torch Linear
 // layout, K contiguous for both GEMM operands), biases / LN params / embeddings f32.
 #include <algorithm>
+#include <type_traits>
 #include <cstdlib>
 
 #include "common.h"
@@ -43,25 +44,29 @@ __device__ __forceinline__ void glds_x4(const void* gsrc, uint32_t lds_addr) {
 // chunks in ascending k, one accumulator) and finished by the same gemm_store4, so a row's
 // result does not depend on which kernel its batch size selected.
 template <int EPI>
+__device__ __forceinline__ float gemm_act(float x) {
+  if constexpr (EPI == EPI_F16_QUICK_GELU) {
+    // x * sigmoid(1.702 x) with hardware exp2 / rcp (~1 ulp each; the result is rounded to
+    // fp16) instead of a full-precision divide
+    return x * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.702f * 1.44269504088896341f * x));
+  } else if constexpr (EPI == EPI_F16_GELU_ERF) {
+    return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));
+  } else {
+    return x;
+  }
+}
+
+// Finish four consecutive outputs C[m][n .. n + 3] = epilogue(v + bias) (K3).
+template <int EPI>
 __device__ __forceinline__ void gemm_store4(const GemmArgs& g, int m, int n, f32x4 v, const float* bn) {
+  typedef _Float16 half4 __attribute__((ext_vector_type(4)));
 #pragma unroll
   for (int r = 0; r < 4; ++r) v[r] += bn[r];
   const size_t o = (size_t)m * g.ldc + n;
   if constexpr (EPI == EPI_F16 || EPI == EPI_F16_QUICK_GELU || EPI == EPI_F16_GELU_ERF) {
-    typedef _Float16 half4 __attribute__((ext_vector_type(4)));
     half4 h;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      float x = v[r];
-      if constexpr (EPI == EPI_F16_QUICK_GELU) {
-        // x * sigmoid(1.702 x) with hardware exp2 / rcp (~1 ulp each; the result is
-        // rounded to fp16) instead of a full-precision divide
-        x = x * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.702f * 1.44269504088896341f * x));
-      } else if constexpr (EPI == EPI_F16_GELU_ERF) {
-        x = 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));
-      }
-      h[r] = (_Float16)x;
-    }
+    for (int r = 0; r < 4; ++r) h[r] = (_Float16)gemm_act<EPI>(v[r]);
     *(half4*)((_Float16*)g.C + o) = h;
   } else if constexpr (EPI == EPI_F32_RESIDUAL) {
     f32x4* p = (f32x4*)((float*)g.C + o);
@@ -71,6 +76,41 @@ __device__ __forceinline__ void gemm_store4(const GemmArgs& g, int m, int n, f32
     *p = c;
   } else {
     *(f32x4*)((float*)g.C + o) = v;
+  }
+}
+
+// Eight consecutive outputs C[m][n .. n + 7] (K3d): one 16-byte store for the f16
+// epilogues, two for the f32 ones — the same per-element arithmetic as gemm_store4.
+template <int EPI>
+__device__ __forceinline__ void gemm_store8(const GemmArgs& g, int m, int n, f32x4 v0, f32x4 v1, const float* bn) {
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    v0[r] += bn[r];
+    v1[r] += bn[4 + r];
+  }
+  const size_t o = (size_t)m * g.ldc + n;
+  if constexpr (EPI == EPI_F16 || EPI == EPI_F16_QUICK_GELU || EPI == EPI_F16_GELU_ERF) {
+    half8 h;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      h[r] = (_Float16)gemm_act<EPI>(v0[r]);
+      h[4 + r] = (_Float16)gemm_act<EPI>(v1[r]);
+    }
+    *(half8*)((_Float16*)g.C + o) = h;
+  } else if constexpr (EPI == EPI_F32_RESIDUAL) {
+    f32x4* p = (f32x4*)((float*)g.C + o);
+    f32x4 c0 = p[0], c1 = p[1];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      c0[r] += v0[r];
+      c1[r] += v1[r];
+    }
+    p[0] = c0;
+    p[1] = c1;
+  } else {
+    f32x4* p = (f32x4*)((float*)g.C + o);
+    p[0] = v0;
+    p[1] = v1;
   }
 }
 
@@ -179,9 +219,9 @@ __global__ __launch_bounds__(GTHREADS) void gemm_nt_kernel(GemmArgs g) {
 }
 
 // ---------------------------------------------------------------------------
-// K3d (M >= 1024, N % 256 == 0: the ViT batches): 256 x 256 x 64 tiles, 8 waves (2 M x 4 N,
-// 128 x 64 each), an eight-phase pipeline whose LDS-DMA prefetch stays in flight across
-// barriers, and two wave groups in ping-pong.
+// K3d (M >= 1024, N % 256 == 0: the ViT batches): persistent, one workgroup per CU, 256 x 256
+// x 64 tiles, 8 waves (2 M x 4 N, 128 x 64 each), an eight-phase pipeline whose LDS-DMA
+// prefetch stays in flight across barriers and across tiles, two wave groups in ping-pong.
 //
 // A K-tile is staged as four 16 KiB half-tiles ("slots"), each 128 LDS rows x 128 B:
 //   slot 0 A-h0: tile rows {0..63, 128..191}   slot 1 B-h0: tile cols {64w + 0..31}
@@ -191,10 +231,13 @@ __global__ __launch_bounds__(GTHREADS) void gemm_nt_kernel(GemmArgs g) {
 // one new slot (phase 0 also B-h0): A-h0 + B-h0 -> (h0, hh0); B-h1 -> (h0, hh1); A-h1 ->
 // (h1, hh1); nothing -> (h1, hh0). A slot is dead after its only read phase and is restaged
 // one phase later with the K-tile two ahead (two LDS buffers x four slots = 128 KiB).
-// Load sequence L[i] = slot (i & 3) of K-tile i >> 2; phase phi = 4t + p issues L[phi + 7]
-// (the prologue issues L[0..6]) and waits until L[phi + 2] has landed — what phase phi + 1
-// reads — leaving the five younger half-tiles (10 LDS-DMA instructions per wave) in flight:
-// one counted `s_waitcnt vmcnt`, never 0 in the loop.
+// Load stream L[i] = slot (i & 3) of the workgroup's (i >> 2)-th K-tile, counted over all
+// its tiles; phase phi issues L[phi + 7] (the prologue L[0..6]) and waits until L[phi + 2]
+// has landed — what phase phi + 1 reads — leaving the five younger half-tiles (10 LDS-DMA
+// instructions per wave) in flight: one counted `s_waitcnt vmcnt`, never 0 in the loop.
+// The epilogue of a tile (32 vector stores per wave) therefore runs while the next tile's
+// first half-tiles land, and its stores drain under the next tile's MFMAs: the five waits
+// after it count the stores among the younger operations.
 // Phase: ds_reads -> issue -> vmcnt(N) + lgkmcnt(0) -> s_barrier -> MFMAs (setprio 1) ->
 // s_barrier, with the two wave groups one barrier apart (ping-pong: on every SIMD one
 // wave's MFMA segment overlaps the other wave's read segment). A wave's reads of phase phi
@@ -202,64 +245,119 @@ __global__ __launch_bounds__(GTHREADS) void gemm_nt_kernel(GemmArgs g) {
 // issuing phase phi + 1's LDS-DMA (WAR: a slot may be restaged one phase after its read);
 // the vmcnt waits of phase phi precede the barrier ending the later group's read segment,
 // which precedes every read of phase phi + 1 (RAW).
+// Tiles: XCD x (blocks b = x mod 8) owns a contiguous range of tile ids (tm-major), taken
+// round-robin by its workgroups, so an A panel and the weight panels stay in that L2.
 constexpr int G8_BM = 256, G8_BN = 256, G8_THREADS = 512;
 constexpr int G8_SLOT = 16384;
+constexpr int G8_BIAS_MAX = 4096;  // bias floats staged in LDS
 
-__device__ __forceinline__ void g8_wait_vm(int younger_halves) {
-  switch (younger_halves) {  // wave-uniform: 2 LDS-DMA instructions per half-tile
-    case 5: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
-    case 4: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
-    case 3: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
-    case 2: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
-    case 1: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+#define MRAG_VMCNT_CASE(n) \
+  case n: asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory"); break;
+__device__ __forceinline__ void vmcnt_wait(int n) {  // n wave-uniform, even, 0..42
+  switch (n) {
+    MRAG_VMCNT_CASE(2) MRAG_VMCNT_CASE(4) MRAG_VMCNT_CASE(6) MRAG_VMCNT_CASE(8) MRAG_VMCNT_CASE(10)
+    MRAG_VMCNT_CASE(12) MRAG_VMCNT_CASE(14) MRAG_VMCNT_CASE(16) MRAG_VMCNT_CASE(18) MRAG_VMCNT_CASE(20)
+    MRAG_VMCNT_CASE(22) MRAG_VMCNT_CASE(24) MRAG_VMCNT_CASE(26) MRAG_VMCNT_CASE(28) MRAG_VMCNT_CASE(30)
+    MRAG_VMCNT_CASE(32) MRAG_VMCNT_CASE(34) MRAG_VMCNT_CASE(36) MRAG_VMCNT_CASE(38) MRAG_VMCNT_CASE(40)
+    MRAG_VMCNT_CASE(42)
     default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
   }
 }
+#undef MRAG_VMCNT_CASE
 
 // ABL (timing experiments only, wrong results): 1 = no LDS-DMA in the loop, 2 = no
-// fragment ds_reads in the loop, 3 = both, 4 = no ping-pong stagger
+// fragment ds_reads in the loop, 3 = both, 4 = no ping-pong stagger, 5 = LDS-DMA from the
+// first two K-tiles only (L2-hot), 7 = no epilogue stores
 template <int EPI, int ABL = 0>
 __global__ __launch_bounds__(G8_THREADS) void gemm_8p_kernel(GemmArgs g) {
-  __shared__ __attribute__((aligned(16))) char smem[8 * G8_SLOT];
+  __shared__ __attribute__((aligned(16))) char smem[8 * G8_SLOT + (ABL == 8 ? 16 : G8_BIAS_MAX * 4)];
+  float* sbias = (float*)(smem + 8 * G8_SLOT);
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wr = w >> 2, wc = w & 3;
   const int fr = lane & 15, fq = lane >> 4;
   const uint32_t lds_base = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)((AS3 char*)smem));
 
+  // this workgroup's tiles: lo + s + k * nbx, k = 0 .. my_n - 1
   const int tiles_n = g.N / G8_BN;
-  const int t = xcd_remap(blockIdx.x, gridDim.x);
-  const int tm = t / tiles_n, tn = t - (t / tiles_n) * tiles_n;
-  const int m0 = tm * G8_BM, n0 = tn * G8_BN;
-  const int total = (g.K / GK) * 4;  // half-tiles
+  const int ntiles = ((g.M + G8_BM - 1) / G8_BM) * tiles_n;
+  const int xcd = blockIdx.x & 7, sidx = blockIdx.x >> 3;
+  const int nbx = ((int)gridDim.x - xcd + 7) >> 3;
+  const int q8 = ntiles >> 3, r8 = ntiles & 7;
+  const int lo = xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8;
+  const int cnt = q8 + (xcd < r8 ? 1 : 0);
+  const int my_n = sidx < cnt ? (cnt - sidx + nbx - 1) / nbx : 0;
+  if (my_n == 0) return;  // whole workgroup, before any barrier
+
+  if constexpr (ABL != 8) {
+    for (int i = threadIdx.x; i < g.N; i += G8_THREADS) sbias[i] = g.bias ? g.bias[i] : 0.f;
+    __syncthreads();
+  }
+
+  const int ktiles = g.K / GK;
+  const int KH = 4 * ktiles;       // half-tiles per tile
+  const int total = my_n * KH;     // half-tiles of the whole stream
 
   // staging: this wave fills pieces 2w, 2w + 1 (8 LDS rows each) of every slot; LDS row
   // j = 16 w + 8 q + (lane >> 3), chunk position lane & 7 holds source chunk
   // (lane & 7) ^ ((j >> 1) & 7)
-  const _Float16* srcA[2][2];
-  const _Float16* srcB[2][2];
+  int rowA[2][2], colB[2][2], coffq[2];
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
     const int j = 16 * w + 8 * q + (lane >> 3);
-    const int c = (lane & 7) ^ ((j >> 1) & 7);
+    coffq[q] = ((lane & 7) ^ ((j >> 1) & 7)) * 8;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      const int row = (j & 63) + 128 * (j >> 6) + 64 * h;
-      srcA[h][q] = g.A + (size_t)min(m0 + row, g.M - 1) * g.lda + c * 8;
-      const int col = 64 * (j >> 5) + 32 * h + (j & 31);
-      srcB[h][q] = g.W + (size_t)(n0 + col) * g.ldw + c * 8;
+      rowA[h][q] = (j & 63) + 128 * (j >> 6) + 64 * h;
+      // LDS row 32 wc + 16 jb + 4 f + r (f, r < 4) holds tile column 64 wc + 32 h + 8 f + 4 jb + r,
+      // so lane group f of a 16x16 block pair (jb = 0, 1) owns 8 consecutive columns
+      const int jj = j & 31;
+      colB[h][q] = 64 * (j >> 5) + 32 * h + 8 * ((jj >> 2) & 3) + 4 * (jj >> 4) + (jj & 3);
     }
   }
-  auto stage = [&](int i) {  // L[i]: slot i & 3 of K-tile i >> 2
-    const int kt = i >> 2, sl = i & 3;
-    const int k0 = kt * GK;
-    const uint32_t dst = lds_base + (uint32_t)(((kt & 1) * 4 + sl) * G8_SLOT) + (uint32_t)(w * 2048);
+  // The stream is consumed strictly in order (prologue L[0..6], then L[phi + 7]); phase p of
+  // a K-tile always issues slot (p + 3) & 3, a compile-time constant, so the loader keeps
+  // its K-tile position incrementally and recomputes this lane's source-row element
+  // offsets once per tile (no per-phase division or slot selection).
+  int ld_kt = 0, ld_par = 0, ld_T = lo + sidx;
+  int gA[2][2], gB[2][2];  // element offsets (row * ld + chunk) for the tile being loaded
+  auto load_tile_offsets = [&]() {
+    const int tm = ld_T / tiles_n;
+    const int m0 = tm * G8_BM, n0 = (ld_T - tm * tiles_n) * G8_BN;
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        gA[h][q] = min(m0 + rowA[h][q], g.M - 1) * g.lda + coffq[q];
+        gB[h][q] = (n0 + colB[h][q]) * g.ldw + coffq[q];
+      }
+  };
+  load_tile_offsets();
+  auto stage_slot = [&](auto SL) {
+    constexpr int sl = decltype(SL)::value;
+    const int k0 = (ABL == 5 ? (ld_kt & 1) : ld_kt) * GK;
+    const uint32_t dst = lds_base + (uint32_t)((ld_par * 4 + sl) * G8_SLOT) + (uint32_t)(w * 2048);
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
-      const _Float16* src = (sl == 0) ? srcA[0][q] : (sl == 1) ? srcB[0][q] : (sl == 2) ? srcB[1][q] : srcA[1][q];
+      const _Float16* src = (sl == 0)   ? g.A + gA[0][q]
+                            : (sl == 1) ? g.W + gB[0][q]
+                            : (sl == 2) ? g.W + gB[1][q]
+                                        : g.A + gA[1][q];
       glds_x4(src + k0, dst + q * 1024);
     }
+    if constexpr (sl == 3) {  // K-tile complete: advance the loader
+      ld_par ^= 1;
+      if (++ld_kt == ktiles) {
+        ld_kt = 0;
+        ld_T += nbx;
+        load_tile_offsets();
+      }
+    }
   };
+  using S0 = std::integral_constant<int, 0>;
+  using S1 = std::integral_constant<int, 1>;
+  using S2 = std::integral_constant<int, 2>;
+  using S3 = std::integral_constant<int, 3>;
 
   int offA[4][2], offB[2][2];
 #pragma unroll
@@ -271,15 +369,6 @@ __global__ __launch_bounds__(G8_THREADS) void gemm_8p_kernel(GemmArgs g) {
   }
 
   f32x4 acc[2][2][4][2];  // [h][hh][i][jb]
-#pragma unroll
-  for (int h = 0; h < 2; ++h)
-#pragma unroll
-    for (int hh = 0; hh < 2; ++hh)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int jb = 0; jb < 2; ++jb) acc[h][hh][i][jb] = f32x4{};
-
   half8 fa[4][2], fb0[2][2], fb1[2][2];
   auto readA = [&](const char* slot) {
 #pragma unroll
@@ -315,66 +404,104 @@ __global__ __launch_bounds__(G8_THREADS) void gemm_8p_kernel(GemmArgs g) {
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
   };
-  // end of a read segment: issue L[phi + 7], wait for L[phi + 2] (read by phase phi + 1)
-  // and for this segment's own ds_reads, barrier
-  auto end_reads = [&](int phi) {
-    if (ABL != 1 && ABL != 3 && phi + 7 < total) stage(phi + 7);
-    g8_wait_vm(min(5, max(0, total - 1 - (phi + 2))));
+  int st_phi = -100;  // last phase before the most recent epilogue
+  int st_cnt = 0;     // vector stores that epilogue issued (wave-uniform)
+  // end of a read segment: issue L[phi + 7] (slot SL), wait for L[phi + 2] (read by phase
+  // phi + 1) and for this segment's own ds_reads, barrier
+  auto end_reads = [&](int phi, auto SL) {
+    const bool full = phi + 7 < total;  // five younger half-tiles in flight
+    if (ABL != 1 && ABL != 3 && full) stage_slot(SL);
+    const bool post = phi - st_phi <= 5;  // the last epilogue's stores are younger than L[phi + 2]
+    if (__builtin_expect(full && !post, 1)) {
+      asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+    } else if (full && st_cnt == 32) {
+      asm volatile("s_waitcnt vmcnt(42)" ::: "memory");
+    } else if (full && st_cnt == 16) {
+      asm volatile("s_waitcnt vmcnt(26)" ::: "memory");
+    } else {
+      vmcnt_wait(2 * min(5, max(0, total - 1 - (phi + 2))) + (post ? st_cnt : 0));
+    }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     bar();
   };
 
   {  // prologue: L[0..6], then L[0], L[1] landed
     const int last = min(6, total - 1);
-    for (int i = 0; i <= last; ++i) stage(i);
-    g8_wait_vm(min(5, max(0, total - 2)));
+    stage_slot(S0{});
+    if (last >= 1) stage_slot(S1{});
+    if (last >= 2) stage_slot(S2{});
+    if (last >= 3) stage_slot(S3{});
+    if (last >= 4) stage_slot(S0{});
+    if (last >= 5) stage_slot(S1{});
+    if (last >= 6) stage_slot(S2{});
+    vmcnt_wait(2 * min(5, max(0, total - 2)));
     bar();
   }
   // waves 4..7 (one per SIMD beside a wave of 0..3) run one barrier behind waves 0..3
   if (ABL != 4 && wr == 1) bar();
-  const int ktiles = total >> 2;
-  for (int kt = 0; kt < ktiles; ++kt) {
-    const char* buf = (const char*)smem + (kt & 1) * 4 * G8_SLOT;
-    const int phi = 4 * kt;
-    readA(buf + 0 * G8_SLOT);  // phase 0: (h0, hh0)
-    readB(buf + 1 * G8_SLOT, fb0);
-    end_reads(phi);
-    mfma_q(acc[0][0], fb0);
-    bar();
-    readB(buf + 2 * G8_SLOT, fb1);  // phase 1: (h0, hh1)
-    end_reads(phi + 1);
-    mfma_q(acc[0][1], fb1);
-    bar();
-    readA(buf + 3 * G8_SLOT);  // phase 2: (h1, hh1)
-    end_reads(phi + 2);
-    mfma_q(acc[1][1], fb1);
-    bar();
-    end_reads(phi + 3);  // phase 3: (h1, hh0) from registers
-    mfma_q(acc[1][0], fb0);
-    bar();
-  }
-  if (ABL != 4 && wr == 0) bar();  // same barrier count for both groups
+  int phi = 0;
+  for (int tl = 0; tl < my_n; ++tl) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int jb = 0; jb < 2; ++jb) acc[h][hh][i][jb] = f32x4{};
+    for (int kt = 0; kt < ktiles; ++kt, phi += 4) {
+      const char* buf = (const char*)smem + ((phi >> 2) & 1) * 4 * G8_SLOT;
+      readA(buf + 0 * G8_SLOT);  // phase 0: (h0, hh0)
+      readB(buf + 1 * G8_SLOT, fb0);
+      end_reads(phi, S3{});
+      mfma_q(acc[0][0], fb0);
+      bar();
+      readB(buf + 2 * G8_SLOT, fb1);  // phase 1: (h0, hh1)
+      end_reads(phi + 1, S0{});
+      mfma_q(acc[0][1], fb1);
+      bar();
+      readA(buf + 3 * G8_SLOT);  // phase 2: (h1, hh1)
+      end_reads(phi + 2, S1{});
+      mfma_q(acc[1][1], fb1);
+      bar();
+      end_reads(phi + 3, S2{});  // phase 3: (h1, hh0) from registers
+      mfma_q(acc[1][0], fb0);
+      bar();
+    }
+    st_phi = phi - 1;
+    st_cnt = 0;
 
-  // epilogue: block (h, hh, i, jb): row 128 wr + 64 h + 16 i + fr, columns
-  // 64 wc + 32 hh + 16 jb + 4 fq + (0..3)
+    // epilogue: blocks (h, hh, i, jb = 0, 1): row 128 wr + 64 h + 16 i + fr, columns
+    // 64 wc + 32 hh + 8 fq + 4 jb + (0..3): one 16-byte f16 store (two for f32) per lane
+    const int T = lo + sidx + tl * nbx;
+    const int tm = T / tiles_n;
+    const int m0 = tm * G8_BM, n0 = (T - tm * tiles_n) * G8_BN;
+    constexpr int SPB = (EPI == EPI_F32_RESIDUAL || EPI == EPI_F32) ? 2 : 1;  // stores per block
 #pragma unroll
-  for (int hh = 0; hh < 2; ++hh) {
+    for (int hh = 0; hh < 2; ++hh) {
+      const int n = n0 + 64 * wc + 32 * hh + 8 * fq;
+      float bn[8];
 #pragma unroll
-    for (int jb = 0; jb < 2; ++jb) {
-      const int n = n0 + 64 * wc + 32 * hh + 16 * jb + 4 * fq;
-      float bn[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) bn[r] = g.bias ? g.bias[n + r] : 0.f;
+      for (int r = 0; r < 8; ++r) bn[r] = ABL == 8 ? 0.f : sbias[n + r];
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const int m = m0 + 128 * wr + 64 * h + 16 * i + fr;
-          if (m < g.M) gemm_store4<EPI>(g, m, n, acc[h][hh][i][jb], bn);
+          const int mb = m0 + 128 * wr + 64 * h + 16 * i;  // wave-uniform block row
+          const int m = mb + fr;
+          if constexpr (ABL == 7) {
+            asm volatile("" ::"v"(acc[h][hh][i][0]), "v"(acc[h][hh][i][1]), "v"(bn[0]));
+          } else if (mb < g.M) {  // uniform branch: a block with a valid row issues exactly
+            st_cnt += SPB;        // SPB vector stores (counted for the vmcnt bookkeeping)
+            if (m < g.M) {
+              gemm_store8<EPI>(g, m, n, acc[h][hh][i][0], acc[h][hh][i][1], bn);
+            }
+          }
         }
       }
     }
   }
+  if (ABL != 4 && wr == 0) bar();  // same barrier count for both groups
 }
 
 // ---------------------------------------------------------------------------
@@ -720,8 +847,30 @@ int gemm_big_mode() {
   return v;
 }
 
+int num_cus() {
+  static int n = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      v = 256;
+    return v;
+  }();
+  return n;
+}
+
 int launch_gemm_8p(const GemmArgs& g, int epi, hipStream_t s) {
-  const dim3 grid((unsigned)(((g.M + G8_BM - 1) / G8_BM) * (g.N / G8_BN)));
+  const int ntiles = ((g.M + G8_BM - 1) / G8_BM) * (g.N / G8_BN);
+  int nb = std::min((ntiles + 7) / 8 * 8, std::max(8, num_cus() / 8 * 8));
+  static const int grid_override = [] {
+    const char* e = getenv("MRAG_G8_GRID");
+    return e ? atoi(e) : 0;
+  }();
+  if (grid_override > 0) nb = std::min(nb, grid_override);
+  static bool said = false;
+  if (!said && getenv("MRAG_G8_VERBOSE")) {
+    fprintf(stderr, "K3d: %d CUs, grid %d for %d tiles\n", num_cus(), nb, ntiles);
+    said = true;
+  }
+  const dim3 grid((unsigned)nb);
   static const int abl = [] {
     const char* e = getenv("MRAG_GEMM_ABL");
     return e ? atoi(e) : 0;
@@ -731,6 +880,9 @@ int launch_gemm_8p(const GemmArgs& g, int epi, hipStream_t s) {
       case 1: hipLaunchKernelGGL((gemm_8p_kernel<EPI_F16, 1>), grid, dim3(G8_THREADS), 0, s, g); break;
       case 2: hipLaunchKernelGGL((gemm_8p_kernel<EPI_F16, 2>), grid, dim3(G8_THREADS), 0, s, g); break;
       case 3: hipLaunchKernelGGL((gemm_8p_kernel<EPI_F16, 3>), grid, dim3(G8_THREADS), 0, s, g); break;
+      case 5: hipLaunchKernelGGL((gemm_8p_kernel<EPI_F16, 5>), grid, dim3(G8_THREADS), 0, s, g); break;
+      case 7: hipLaunchKernelGGL((gemm_8p_kernel<EPI_F16, 7>), grid, dim3(G8_THREADS), 0, s, g); break;
+      case 8: hipLaunchKernelGGL((gemm_8p_kernel<EPI_F16, 8>), grid, dim3(G8_THREADS), 0, s, g); break;
       default: hipLaunchKernelGGL((gemm_8p_kernel<EPI_F16, 4>), grid, dim3(G8_THREADS), 0, s, g); break;
     }
     MRAG_CHECK_LAUNCH();
@@ -753,7 +905,7 @@ int launch_gemm(const GemmArgs& g, int epi, hipStream_t s) {
   MRAG_REQUIRE(g.N % GN == 0 && g.K % GK == 0, "gemm: N=%d must be a multiple of %d and K=%d of %d", g.N, GN, g.K,
                GK);
   MRAG_REQUIRE(g.lda % 8 == 0 && g.ldw % 8 == 0 && g.ldc % 4 == 0, "gemm: lda/ldw must be multiples of 8, ldc of 4");
-  if (gemm_big_mode() != 0 && g.M >= 1024 && g.N % G8_BN == 0) return launch_gemm_8p(g, epi, s);
+  if (gemm_big_mode() != 0 && g.M >= 1024 && g.N % G8_BN == 0 && g.N <= G8_BIAS_MAX) return launch_gemm_8p(g, epi, s);
   const dim3 grid((unsigned)(((g.M + GM - 1) / GM) * (g.N / GN)));
   switch (epi) {
     case EPI_F16: hipLaunchKernelGGL(gemm_nt_kernel<EPI_F16>, grid, dim3(GTHREADS), 0, s, g); break;

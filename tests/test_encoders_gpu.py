@@ -65,11 +65,12 @@ def test_gemm_epilogues(cuda, epi):
     assert err < 1e-2, err
 
 
-@pytest.mark.parametrize("M,N,K", [(1100, 768, 768), (2048, 384, 320), (1024, 2304, 192)])
+@pytest.mark.parametrize("M,N,K", [(1100, 768, 768), (2048, 384, 320), (1024, 2304, 192), (8300, 2304, 128)])
 @pytest.mark.parametrize("epi", [0, 1, 2, 3, 4])
 def test_gemm_big_tiles(cuda, M, N, K, epi):
-    """K3b (256-row tiles, used from M = 1024): ragged M (1100 = 4 x 256 + 76), both tile
-    widths (N % 256 == 0 -> 256, else 128), every epilogue; same tolerance as K3."""
+    """K3d (persistent 256 x 256 tiles, used from M = 1024 when N % 256 == 0; K3 otherwise):
+    ragged M (1100 = 4 x 256 + 76, 8300), 297 tiles (> one per CU: the load stream and the
+    epilogue stores run across tiles), every epilogue; same tolerance as K3."""
     import torch
 
     from app.encoders import gemm_nt
