@@ -171,6 +171,99 @@ def clip_leg(steps: int, warmup: int):
     return bench_clip_images(steps=steps, warmup=warmup)
 
 
+FUSION_ROWS_PER_GPU = 1 << 19  # config 5: 4M text + 4M image rows over 8 GPUs
+FUSION_T = 16                   # synthetic query length (tokens, incl. specials)
+
+
+def fusion_leg(world: int, rank: int, local: int, steps: int, warmup: int):
+    """BASELINE config 5: mixed text+image retrieval of a 1000-query batch, end to end on
+    the GPUs: both query towers (MiniLM-L6 -> 384-d, CLIP text -> 512-d) on synthetic token
+    ids, each rank encoding its slice of the batch (all-gathered over RCCL at N > 1), then
+    the text (k = 50) and image (k = 12) searches over row-sharded corpora of 2^19 x 384 +
+    2^19 x 512 rows per GPU (4M + 4M at 8 GPUs) with the per-shard all-gather + merge, and
+    the reference's z-score fusion (rerank off, final_n = 4) on rank 0
+    (app.retrieval.fuse_scores, vectorised). value = queries/s over the whole corpus."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from app.encoders import CLIP_TEXT_B32, MINILM_L6, GpuEncoder
+    from app.retrieval import fuse_scores
+    from app.settings import settings
+    from app.vector_store import FlatIndex
+    from app.vector_store.sharded import ShardedFlatIndex
+
+    dev = torch.device("cuda", local)
+    kt, ki = settings.retrieval.index_topk_text, settings.retrieval.index_topk_image
+    final_n = settings.retrieval.final_n
+    shards = []
+    for dim, seed in ((MINILM_L6.hidden, 2000), (CLIP_TEXT_B32.proj_dim, 3000)):
+        g = torch.Generator(device=dev).manual_seed(seed + rank)
+        x = torch.randn((FUSION_ROWS_PER_GPU, dim), generator=g, device=dev)
+        ix = FlatIndex(dim, device=local)
+        ix.add(x)
+        del x
+        shards.append(ShardedFlatIndex(ix, row_offset=rank * FUSION_ROWS_PER_GPU))
+    torch.cuda.empty_cache()
+    text_sh, img_sh = shards
+    gq = torch.Generator(device=dev).manual_seed(7)  # same batch on every rank
+    ids_m = torch.randint(1000, 30000, (NQ, FUSION_T), generator=gq, device=dev, dtype=torch.int32)
+    ids_m[:, 0], ids_m[:, -1] = 101, 102  # [CLS] ... [SEP]
+    mask = torch.ones_like(ids_m)
+    ids_c = torch.randint(1, 49405, (NQ, FUSION_T), generator=gq, device=dev, dtype=torch.int32)
+    ids_c[:, 0], ids_c[:, -1] = 49406, 49407  # <|startoftext|> ... <|endoftext|>
+    per = (NQ + world - 1) // world
+    lo, hi = rank * per, min(NQ, (rank + 1) * per)
+    minilm = GpuEncoder(MINILM_L6, device=local)
+    clipt = GpuEncoder(CLIP_TEXT_B32, device=local)
+
+    def gather(v):
+        if world == 1:
+            return v
+        buf = torch.zeros((per, v.shape[1]), dtype=v.dtype, device=dev)
+        buf[: v.shape[0]] = v
+        out = torch.empty((world * per, v.shape[1]), dtype=v.dtype, device=dev)
+        dist.all_gather_into_tensor(out, buf)
+        return out[:NQ]
+
+    def step():
+        tv = gather(minilm.embed_tokens(ids_m[lo:hi], mask[lo:hi]))
+        iv = gather(clipt.embed_tokens(ids_c[lo:hi]))
+        st, rt = text_sh.search(tv, kt)
+        si, ri = img_sh.search(iv, ki)
+        if rank == 0:
+            pick, _ = fuse_scores(st.cpu().numpy(), si.cpu().numpy(), final_n)
+            return pick
+        return None
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    _barrier(world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        pick = step()
+    torch.cuda.synchronize()
+    _barrier(world)
+    dt = _max_over_ranks(time.perf_counter() - t0, world)
+    if rank != 0:
+        return None
+    return {
+        "metric": "mixed text+image retrieve queries/s (BASELINE config 5)",
+        "value": round(NQ * steps / dt, 1),
+        "unit": "queries/s (each query: MiniLM + CLIP-text encode, text top-50 + image top-12 over the whole "
+                "sharded corpus, z-score fusion to 4)",
+        "steps": steps,
+        "ms_per_step": round(dt / steps * 1e3, 3),
+        "workload": f"{NQ} synthetic {FUSION_T}-token queries; corpora {FUSION_ROWS_PER_GPU} x 384 text + "
+                    f"{FUSION_ROWS_PER_GPU} x 512 image rows per GPU ({world * FUSION_ROWS_PER_GPU} + "
+                    f"{world * FUSION_ROWS_PER_GPU} total), synthetic weights, rerank off",
+        "top_k": {"text": kt, "image": ki, "final_n": final_n},
+        "fused_hits_last_step": int((pick >= 0).sum()),
+    }
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -178,6 +271,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-clip", action="store_true")
+    ap.add_argument("--no-fusion", action="store_true")
     args = ap.parse_args()
 
     import torch
@@ -231,6 +325,13 @@ def main():
     flops_per_launch = 2.0 * NQ * ROWS_PER_GPU * DIM
     achieved_tflops = flops_per_launch / avg_scan_s / 1e12 if avg_scan_s > 0 else 0.0
 
+    fusion = None
+    if not args.no_fusion:  # config 5 (all ranks take part: sharded corpora + all-gathers)
+        del sharded
+        index.close()
+        torch.cuda.empty_cache()
+        fusion = fusion_leg(world, rank, local, steps=max(5, args.steps // 2), warmup=2)
+
     if rank == 0:
         out = {
             "metric": "CLIP img-embeds/sec/GPU; kNN queries/sec on 1M×512 at top-k=10, 1/2/4/8 GPUs",
@@ -275,6 +376,8 @@ def main():
                 if not args.no_cpu_baseline:
                     clip["cpu_baseline"] = clip_cpu_baseline()
                 out["clip"] = clip
+        if fusion is not None:
+            out["fusion"] = fusion
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline()
         print(json.dumps(out), flush=True)

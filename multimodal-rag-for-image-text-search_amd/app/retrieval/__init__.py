@@ -81,4 +81,59 @@ def retrieve_batch(user_id: str, queries: Sequence[str], top_k_text: Optional[in
     return out
 
 
-__all__ = ["search_batch", "retrieve_batch"]
+def _z_rows(scores64: np.ndarray, valid: np.ndarray) -> np.ndarray:
+    """``_z_scores`` (app/ml/retrieve.py:185-194) of every row's valid prefix: float32 mean
+    and std of the list (numpy's own reductions, rows of equal length grouped so each group
+    is one contiguous 2-D reduction = the per-list 1-D one), then (v - mean) / std in f64
+    on the f64 score; a zero std gives zeros."""
+    q, k = scores64.shape
+    z = np.zeros((q, k), dtype=np.float64)
+    counts = valid.sum(axis=1)
+    for n in np.unique(counts):
+        if n == 0:
+            continue
+        rows = np.nonzero(counts == n)[0]
+        v = scores64[rows, :n]
+        arr = v.astype(np.float32)
+        mean = arr.mean(axis=1).astype(np.float64)[:, None]
+        std = arr.std(axis=1).astype(np.float64)[:, None]
+        with np.errstate(divide="ignore", invalid="ignore"):
+            zz = np.where(std == 0, 0.0, (v - mean) / np.where(std == 0, 1.0, std))
+        z[rows, :n] = zz
+    return z
+
+
+def fuse_scores(text_scores, image_scores, final_n: Optional[int] = None):
+    """Vectorised ``_fuse_results`` with rerank off (app/ml/retrieve.py:158-182) for a batch
+    of queries, on the raw per-query hit scores the flat index returns.
+
+    ``text_scores`` f32 [Q, kt], ``image_scores`` f32 [Q, ki] in hit order (score desc),
+    ``-inf`` marking missing hits (fewer matches than k). Each hit's score is first taken
+    through the drop-in store's path (``1 - f32(1 - s)``, the f64 value a caller sees).
+    Returns (``pick`` int64 [Q, final_n]: index into the concatenated text+image hit list,
+    -1 past the end; ``combined`` f64 [Q, final_n]), ordered as the reference's stable
+    descending sort of text items then image items."""
+    n_final = int(final_n or settings.retrieval.final_n)
+    ts = np.asarray(text_scores, dtype=np.float32)
+    im = np.asarray(image_scores, dtype=np.float32)
+    if ts.ndim != 2 or im.ndim != 2 or ts.shape[0] != im.shape[0]:
+        raise ValueError("expected [Q, kt] and [Q, ki] score arrays")
+    one = np.float32(1.0)
+
+    def caller_scores(s):
+        valid = np.isfinite(s)
+        s64 = 1.0 - (one - np.where(valid, s, np.float32(0))).astype(np.float64)
+        return s64, valid
+
+    t64, tv = caller_scores(ts)
+    i64, iv = caller_scores(im)
+    comb = np.concatenate([_z_rows(t64, tv), _z_rows(i64, iv)], axis=1)
+    valid = np.concatenate([tv, iv], axis=1)
+    key = np.where(valid, -comb, np.inf)  # stable ascending on -score == stable descending sort
+    order = np.argsort(key, axis=1, kind="stable")[:, :n_final]
+    pick = np.where(np.take_along_axis(valid, order, axis=1), order, -1).astype(np.int64)
+    combined = np.where(pick >= 0, np.take_along_axis(comb, order, axis=1), np.nan)
+    return pick, combined
+
+
+__all__ = ["search_batch", "retrieve_batch", "fuse_scores"]

@@ -1437,7 +1437,10 @@ int mrag_knn_search(mrag_knn_index* ix, const float* queries, int64_t nq, int32_
     MRAG_CHECK_LAUNCH();
   } else {
     // v2 (64 queries/wave, KL = 8) unless k is deep enough to want longer per-lane lists
-    const bool use_v2 = k <= 32 && !ix->scan_v1 && (ix->ablate == 0 || ix->ablate >= 10);
+    // (per-lane lists of 8; for 32 < k <= 64 the union of the S split lists still holds
+    // S * 8 >= k + 32 candidates at the batch sizes that matter, and the certificate
+    // sends any query whose top-k a list could not hold to the collect pass)
+    const bool use_v2 = k <= 64 && !ix->scan_v1 && (ix->ablate == 0 || ix->ablate >= 10);
     // query slots: v2 reads every slot of its query group (no lane guard), so pad to a
     // whole group; padding rows are zero (prep) and never reach the output
     const int64_t qpad = use_v2 ? QPG : QPW;

@@ -335,3 +335,37 @@ def test_splitter_algorithm_properties():
     assert all(len(tok(n.text)) <= budget + 4 for n in nodes) and max(len(tok(n.text)) for n in nodes) > budget
     with pytest.raises(ValueError):
         sp.split_text_metadata_aware("a b c", "k: " + " ".join(["v"] * 20))
+
+
+def test_fuse_scores_matches_reference_fusion():
+    """The batched, vectorised fusion (app.retrieval.fuse_scores: BASELINE config 5's last
+    step) equals the drop-in's per-query ``_fuse_results`` — itself pinned against the
+    reference's outputs (golden_fusion.json) — on ragged, tied and constant lists."""
+    from app.ml import retrieve as r
+    from app.retrieval import fuse_scores
+
+    rng = np.random.default_rng(5)
+    Q, kt, ki = 60, 50, 12
+    ts = np.sort(rng.normal(0.3, 0.05, (Q, kt)).astype(np.float32), axis=1)[:, ::-1].copy()
+    im = np.sort(rng.normal(0.2, 0.03, (Q, ki)).astype(np.float32), axis=1)[:, ::-1].copy()
+    ts[3, 20:] = -np.inf  # fewer hits than k
+    im[4, 5:] = -np.inf
+    im[5, :] = -np.inf  # no image hits
+    ts[6, :] = np.float32(0.5)  # zero std -> zeros
+    ts[7, 1:3] = ts[7, 0]  # ties
+    im[8, :] = -np.inf
+    im[8, 0] = np.float32(0.9)  # single hit: std 0
+    pick, comb = fuse_scores(ts, im, final_n=4)
+    for q in range(Q):
+        texts = [{"chunk_id": f"t{j}", "score": 1.0 - float(np.float32(1.0) - s)}
+                 for j, s in enumerate(ts[q]) if np.isfinite(s)]
+        imgs = [{"chunk_id": f"i{j}", "score": 1.0 - float(np.float32(1.0) - s)}
+                for j, s in enumerate(im[q]) if np.isfinite(s)]
+        ref = r._fuse_results(texts, imgs)
+        got = []
+        for p in pick[q]:
+            if p < 0:
+                continue
+            got.append(f"t{p}" if p < kt else f"i{p - kt}")
+        assert got == [e["chunk_id"] for e in ref], q
+        np.testing.assert_array_equal(comb[q][: len(ref)], [e["combined_score"] for e in ref])
