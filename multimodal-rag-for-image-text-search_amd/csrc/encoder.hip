@@ -510,10 +510,9 @@ int mrag_encoder_embed_images(mrag_encoder* e, const uint8_t* images, int32_t ba
   float* X = (float*)e->X.p;
   if (int rc = launch_vit_im2col(img, (_Float16*)e->F16.p, B, S, P, s)) return rc;
   if (int rc = gemm(e->F16.p, e->patch_w.p, nullptr, e->PATCH.p, B * (T - 1), D, Kp, D, EPI_F32, s)) return rc;
-  if (int rc = launch_vit_assemble((const float*)e->PATCH.p, (const float*)e->cls.p, (const float*)e->pos.p, X, B, T,
-                                   D, s))
+  if (int rc = launch_vit_embed_ln((const float*)e->PATCH.p, (const float*)e->cls.p, (const float*)e->pos.p,
+                                   (const float*)e->pre_g.p, (const float*)e->pre_b.p, X, B, T, D, c.ln_eps, s))
     return rc;
-  if (int rc = layernorm(X, nullptr, X, nullptr, e->pre_g, e->pre_b, B * T, D, c.ln_eps, s)) return rc;
   for (int i = 0; i < c.layers; ++i)
     if (int rc = clip_layer(e, e->layers[i], B, T, nullptr, 0, s)) return rc;
   if (int rc = launch_cls_rows(B, T, (int*)e->ROWS.p, s)) return rc;

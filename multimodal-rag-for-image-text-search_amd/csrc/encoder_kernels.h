@@ -46,6 +46,8 @@ int launch_attention(const AttentionArgs& a, int dh, hipStream_t s);
 int launch_vit_im2col(const uint8_t* img, _Float16* out, int B, int S, int P, hipStream_t s);
 int launch_vit_assemble(const float* patch, const float* cls, const float* pos, float* X, int B, int T, int D,
                         hipStream_t s);
+int launch_vit_embed_ln(const float* patch, const float* cls, const float* pos, const float* gamma, const float* beta,
+                        float* X, int B, int T, int D, float eps, hipStream_t s);
 int launch_token_embed(const int32_t* ids, const float* tok, const float* pos, const float* type_tab,
                        const int32_t* types, float* X, int B, int T, int D, int vocab, hipStream_t s);
 int launch_cls_head(const float* pooled, const float* Wc, const float* bc, float* out, int B, int D, int NL,

@@ -545,6 +545,92 @@ __global__ __launch_bounds__(256) void layernorm_kernel(LayerNormArgs a) {
   }
 }
 
+// K2, vectorised (D % 4 == 0, 16-byte aligned rows: every encoder here): one wave per row,
+// lane l owns the float4 chunks l, l + 64, ... (16-byte loads, 16-byte f32 / 8-byte f16
+// stores); two-pass mean / variance in f32 from registers: one HBM pass over the row.
+__device__ __forceinline__ void ln_row4(f32x4 (&v)[4], int lane, int D, float eps, const float* gamma,
+                                        const float* beta, float* y32, _Float16* y16) {
+  typedef _Float16 half4 __attribute__((ext_vector_type(4)));
+  const int nc = D >> 2;  // <= 256 chunks
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) s += (v[j][0] + v[j][1]) + (v[j][2] + v[j][3]);  // v = 0 past the row
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+  const float mean = s / (float)D;
+  float q = 0.f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if (lane + 64 * j < nc) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const float d = v[j][t] - mean;
+        q += d * d;
+      }
+    }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) q += __shfl_xor(q, off);
+  const float rstd = rsqrtf(q / (float)D + eps);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int c = lane + 64 * j;
+    if (c < nc) {
+      const f32x4 g4 = ((const f32x4*)gamma)[c], b4 = ((const f32x4*)beta)[c];
+      f32x4 y;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) y[t] = (v[j][t] - mean) * rstd * g4[t] + b4[t];
+      if (y32) ((f32x4*)y32)[c] = y;
+      if (y16) {
+        half4 h;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) h[t] = (_Float16)y[t];
+        ((half4*)y16)[c] = h;
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void layernorm4_kernel(LayerNormArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= a.rows) return;
+  const int src = a.gather ? a.gather[r] : r;
+  const f32x4* x = (const f32x4*)(a.x + (size_t)src * a.ldx);
+  f32x4 v[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) v[j] = lane + 64 * j < (a.D >> 2) ? x[lane + 64 * j] : f32x4{};
+  ln_row4(v, lane, a.D, a.eps, a.gamma, a.beta, a.y32 ? a.y32 + (size_t)r * a.D : nullptr,
+          a.y16 ? a.y16 + (size_t)r * a.D : nullptr);
+}
+
+// ViT token assembly + pre_layrnorm in one pass (modeling_clip.py:212-217, :642):
+// X[b*T + t] = LN((t == 0 ? cls : patch[b*(T-1) + t-1]) + pos[t])   (f32)
+__global__ __launch_bounds__(256) void vit_embed_ln_kernel(const float* __restrict__ patch,
+                                                           const float* __restrict__ cls,
+                                                           const float* __restrict__ pos, const float* gamma,
+                                                           const float* beta, float* __restrict__ X, int B, int T,
+                                                           int D, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= B * T) return;
+  const int b = r / T, t = r - (r / T) * T;
+  const f32x4* e = (const f32x4*)(t == 0 ? cls : patch + ((size_t)b * (T - 1) + t - 1) * D);
+  const f32x4* p = (const f32x4*)(pos + (size_t)t * D);
+  f32x4 v[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int c = lane + 64 * j;
+    v[j] = f32x4{};
+    if (c < (D >> 2)) {
+      const f32x4 a = e[c], q = p[c];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[j][u] = a[u] + q[u];
+    }
+  }
+  ln_row4(v, lane, D, eps, gamma, beta, X + (size_t)r * D, nullptr);
+}
+
 // ---------------------------------------------------------------------------
 // K4: multi-head attention for sequences up to 512 (K and V of the head f32 in LDS:
 // 2 L dh 4 bytes <= 160 KiB): one workgroup per (sequence, head), each thread takes query
@@ -730,6 +816,144 @@ __global__ __launch_bounds__(256) void attention_mfma64_kernel(AttentionArgs a) 
     }
 }
 
+// K4 v2 (MFMA form, L <= 64, head_dim 64): as v1 up to the softmax, then
+//   O^T = V^T . P^T: P^T is the S^T accumulator itself (registers 8t..8t+7 of key block kb
+//                   are the B fragment of k-step 2kb + t, key order permuted: element j <->
+//                   key 16s + 8(j>>2) + 4h + (j&3)); the V^T A fragments come from the row-major
+//                   V image by ds_read_b64_tr_b16 in that same order (two per fragment, 16 in
+//                   all; v1: 64 ds_read_u16).
+//   The O^T block has the query on the lane and 4 consecutive dims per register group:
+//   16 8-byte stores per lane (v1: 64 scattered 2-byte stores).
+// No block barrier: each wave owns its V image, and a wave past the end returns whole (the
+// transposed read needs EXEC all ones).
+typedef _Float16 half4_t __attribute__((ext_vector_type(4)));
+typedef __fp16 fp16x4_lds __attribute__((__vector_size__(8)));
+
+__device__ __forceinline__ half4_t lds_read_tr16(const _Float16* p) {
+  const fp16x4_lds v = __builtin_amdgcn_ds_read_tr16_b64_v4f16((AS3 fp16x4_lds*)(p));
+  return __builtin_bit_cast(half4_t, v);
+}
+
+__global__ __launch_bounds__(256) void attention_mfma64t_kernel(AttentionArgs a) {
+  constexpr int DH = 64;
+  constexpr int VROW = 96;  // 192-byte rows: the 4 rows of one transposed read hit disjoint banks
+  __shared__ __attribute__((aligned(16))) _Float16 Vs[4][64 * VROW];
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  const int hh = lane >> 5, r = lane & 31;
+  const int pair = blockIdx.x * 4 + w;
+  if (pair >= a.B * a.H) return;
+  const int b = pair / a.H, hd = pair - (pair / a.H) * a.H;
+  const int D = a.H * DH, L = a.L;
+  const size_t rs = (size_t)3 * D;
+  const _Float16* base = a.qkv + (size_t)b * L * rs;
+  _Float16* vs = Vs[w];
+
+  // V rows -> LDS: 8 lanes x 16 B per row, 8 rows per instruction, zero rows >= L
+#pragma unroll
+  for (int it = 0; it < 8; ++it) {
+    const int key = 8 * it + (lane >> 3), c = lane & 7;
+    half8 v = {};
+    if (key < L) v = *(const half8*)(base + (size_t)key * rs + 2 * D + hd * DH + 8 * c);
+    *(half8*)(vs + key * VROW + 8 * c) = v;
+  }
+  // K (A operand) and Q (B operand) fragments: row r + 32*blk, dims 16s + 8hh .. +7
+  half8 kf[2][4], qf[2][4];
+#pragma unroll
+  for (int blk = 0; blk < 2; ++blk) {
+    const int row = r + 32 * blk;
+    const bool ok = row < L;
+    const _Float16* kr = base + (size_t)row * rs + D + hd * DH + 8 * hh;
+    const _Float16* qr = base + (size_t)row * rs + hd * DH + 8 * hh;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      kf[blk][s] = ok ? *(const half8*)(kr + 16 * s) : half8{};
+      qf[blk][s] = ok ? *(const half8*)(qr + 16 * s) : half8{};
+    }
+  }
+  f32x16 st[2][2];  // [key block][query block]
+#pragma unroll
+  for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) {
+      f32x16 acc = {};
+#pragma unroll
+      for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf[kb][s], qf[qb][s], acc, 0, 0, 0);
+      st[kb][qb] = acc;
+    }
+  // softmax over keys for the lane's two queries (as v1); P^T fragments in permuted key order
+  half8 pb[2][4];  // [query block][k-step]
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    const int q = r + 32 * qb;
+    float m = -INFINITY;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) {
+        const int key = (reg & 3) + 8 * (reg >> 2) + 4 * hh + 32 * kb;
+        bool ok = key < L;
+        if (a.mask) ok = ok && a.mask[(size_t)b * L + min(key, L - 1)] != 0;
+        if (a.causal) ok = ok && key <= q;
+        const float v = ok ? st[kb][qb][reg] * a.scale : -INFINITY;
+        st[kb][qb][reg] = v;
+        m = fmaxf(m, v);
+      }
+    m = fmaxf(m, __shfl_xor(m, 32));
+    float l = 0.f;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) {
+        const float pv = m == -INFINITY ? 0.f : __expf(st[kb][qb][reg] - m);
+        st[kb][qb][reg] = pv;
+        l += pv;
+      }
+    l += __shfl_xor(l, 32);
+    const float inv = l > 0.f ? 1.f / l : 0.f;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int kb = s >> 1, t = s & 1;
+      half8 f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] = (_Float16)(st[kb][qb][8 * t + j] * inv);
+      pb[qb][s] = f;
+    }
+  }
+  // V^T fragments: 16-lane group g reads rows (keys) r0 .. r0 + 3, columns (dims) c0 + 4p .. + 3
+  // (lane 4q + p of the group supplies row q); lane i of the group receives dim c0 + i
+  const int g = lane >> 4, q4 = (lane & 15) >> 2, p4 = lane & 3;
+  half8 vf[2][4];  // [dim block][k-step]
+#pragma unroll
+  for (int db = 0; db < 2; ++db)
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const _Float16* pa = vs + (16 * s + 4 * hh + q4) * VROW + 32 * db + 16 * (g & 1) + 4 * p4;
+      const half4_t lo = lds_read_tr16(pa), hi = lds_read_tr16(pa + 8 * VROW);
+      vf[db][s] = half8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    }
+  _Float16* obase = a.out + (size_t)b * L * D + hd * DH;
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    const int q = r + 32 * qb;
+#pragma unroll
+    for (int db = 0; db < 2; ++db) {
+      f32x16 acc = {};
+#pragma unroll
+      for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(vf[db][s], pb[qb][s], acc, 0, 0, 0);
+      // lane: query q, dims 32 db + 8 g4 + 4 hh + (0..3)
+      if (q < L) {
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const half4_t h = {(_Float16)acc[4 * g4], (_Float16)acc[4 * g4 + 1], (_Float16)acc[4 * g4 + 2],
+                             (_Float16)acc[4 * g4 + 3]};
+          *(half4_t*)(obase + (size_t)q * D + 32 * db + 8 * g4 + 4 * hh) = h;
+        }
+      }
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // K1 (prologue): CLIP pixel normalisation fused into the patch im2col.
 // Reference: CLIPImageProcessor rescale (u8 -> f64 * 1/255 -> f32) then (x - mean) / std
@@ -758,6 +982,45 @@ __global__ void vit_im2col_kernel(const uint8_t* __restrict__ img, _Float16* __r
     v8[t] = (_Float16)((x - mean) / stdv);
   }
   *(half8*)(out + row * K + k8) = *(half8*)v8;
+}
+
+// K1 for P = 32 (ViT-B/32), same arithmetic: one thread per (patch, kernel row kh). The 32
+// pixels x 3 channels of one patch row are 96 contiguous bytes (six 16-byte loads); each
+// channel's 32 values are 64 contiguous bytes of the output row (K ordered c, kh, kw): four
+// 16-byte stores per channel. Needs S % 16 == 0 and a 16-byte aligned image base.
+__global__ __launch_bounds__(256) void vit_im2col32_kernel(const uint8_t* __restrict__ img,
+                                                           _Float16* __restrict__ out, int B, int S) {
+  constexpr int P = 32, K = 3 * P * P;
+  const int G = S / P;
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (int64_t)B * G * G * P) return;
+  const int kh = (int)(idx % P);
+  const int64_t row = idx / P;
+  const int b = (int)(row / (G * G)), pidx = (int)(row % (G * G));
+  const int py = pidx / G, px = pidx % G;
+  const uint4* src = (const uint4*)(img + (((size_t)b * S + (size_t)py * P + kh) * S + (size_t)px * P) * 3);
+  union {
+    uint4 v[6];
+    uint8_t u[96];
+  } pix;
+#pragma unroll
+  for (int i = 0; i < 6; ++i) pix.v[i] = src[i];
+  _Float16* dst = out + row * K + kh * P;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const float mean = c == 0 ? 0.48145466f : (c == 1 ? 0.4578275f : 0.40821073f);
+    const float stdv = c == 0 ? 0.26862954f : (c == 1 ? 0.26130258f : 0.27577711f);
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      half8 v8;
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        const float x = (float)((double)pix.u[3 * (8 * h + t) + c] * (1.0 / 255.0));
+        v8[t] = (_Float16)((x - mean) / stdv);
+      }
+      *(half8*)(dst + c * P * P + 8 * h) = v8;
+    }
+  }
 }
 
 // X[b*T + t] = (t == 0 ? cls : patch[b*(T-1) + t-1]) + pos[t]   (f32)
@@ -922,7 +1185,22 @@ int launch_gemm(const GemmArgs& g, int epi, hipStream_t s) {
 int launch_layernorm(const LayerNormArgs& a, hipStream_t s) {
   if (a.rows <= 0) return MRAG_OK;
   MRAG_REQUIRE(a.D > 0 && a.D <= 1024, "layernorm: D=%d unsupported", a.D);
-  hipLaunchKernelGGL(layernorm_kernel, dim3((unsigned)((a.rows + 3) / 4)), dim3(256), 0, s, a);
+  const bool vec4 = a.D % 4 == 0 && a.ldx % 4 == 0 && ((uintptr_t)a.x & 15) == 0 && ((uintptr_t)a.gamma & 15) == 0 &&
+                    ((uintptr_t)a.beta & 15) == 0 && ((uintptr_t)a.y32 & 15) == 0 && ((uintptr_t)a.y16 & 7) == 0;
+  if (vec4)
+    hipLaunchKernelGGL(layernorm4_kernel, dim3((unsigned)((a.rows + 3) / 4)), dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL(layernorm_kernel, dim3((unsigned)((a.rows + 3) / 4)), dim3(256), 0, s, a);
+  MRAG_CHECK_LAUNCH();
+  return MRAG_OK;
+}
+
+int launch_vit_embed_ln(const float* patch, const float* cls, const float* pos, const float* gamma, const float* beta,
+                        float* X, int B, int T, int D, float eps, hipStream_t s) {
+  if (B * T == 0) return MRAG_OK;
+  MRAG_REQUIRE(D % 4 == 0 && D <= 1024, "vit_embed_ln: D=%d unsupported", D);
+  hipLaunchKernelGGL(vit_embed_ln_kernel, dim3((unsigned)((B * T + 3) / 4)), dim3(256), 0, s, patch, cls, pos, gamma,
+                     beta, X, B, T, D, eps);
   MRAG_CHECK_LAUNCH();
   return MRAG_OK;
 }
@@ -952,7 +1230,13 @@ int launch_attention(const AttentionArgs& a, int dh, hipStream_t s) {
                                  160 * 1024));
     attr_set = true;
   }
-  if (dh == 64 && a.L <= 64 && !force_valu_attention()) {
+  static const bool attn_v1 = [] {
+    const char* e = getenv("MRAG_ATTN_V1");
+    return e && atoi(e) == 1;
+  }();
+  if (dh == 64 && a.L <= 64 && !force_valu_attention() && !attn_v1) {
+    hipLaunchKernelGGL(attention_mfma64t_kernel, dim3((unsigned)((a.B * a.H + 3) / 4)), dim3(256), 0, s, a);
+  } else if (dh == 64 && a.L <= 64 && !force_valu_attention()) {
     hipLaunchKernelGGL(attention_mfma64_kernel, dim3((unsigned)((a.B * a.H + 3) / 4)), dim3(256), 0, s, a);
   } else if (dh == 64) {
     hipLaunchKernelGGL(attention_kernel<64>, grid, dim3(threads), shm, s, a);
@@ -968,6 +1252,12 @@ int launch_attention(const AttentionArgs& a, int dh, hipStream_t s) {
 int launch_vit_im2col(const uint8_t* img, _Float16* out, int B, int S, int P, hipStream_t s) {
   const int64_t total8 = (int64_t)B * (S / P) * (S / P) * (3 * P * P / 8);
   if (total8 == 0) return MRAG_OK;
+  if (P == 32 && S % 16 == 0 && ((uintptr_t)img & 15) == 0) {
+    const int64_t n = (int64_t)B * (S / P) * (S / P) * P;
+    hipLaunchKernelGGL(vit_im2col32_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, img, out, B, S);
+    MRAG_CHECK_LAUNCH();
+    return MRAG_OK;
+  }
   hipLaunchKernelGGL(vit_im2col_kernel, dim3((unsigned)((total8 + 255) / 256)), dim3(256), 0, s, img, out, B, S, P);
   MRAG_CHECK_LAUNCH();
   return MRAG_OK;
