@@ -247,19 +247,51 @@ __global__ __launch_bounds__(GTHREADS) void gemm_nt_kernel(GemmArgs g) {
 // which precedes every read of phase phi + 1 (RAW).
 // Tiles: XCD x (blocks b = x mod 8) owns a contiguous range of tile ids (tm-major), taken
 // round-robin by its workgroups, so an A panel and the weight panels stay in that L2.
-constexpr int G8_BM = 256, G8_BN = 256, G8_THREADS = 512;
-constexpr int G8_SLOT = 16384;
+constexpr int G8_THREADS = 512;
+constexpr int G8_BUF = 65536;      // one K-tile: two A and two B half-tile slots
 constexpr int G8_BIAS_MAX = 4096;  // bias floats staged in LDS
+
+// Tile geometry. CFG 0: 256 x 256 tiles (waves of 128 x 64). CFG 1: 128 x 384 tiles (waves of
+// 64 x 96) for N = 768 (out-proj, fc2 of ViT-B/32): 200 tiles instead of 150 on 256 CUs, one
+// round of 3/4-size tiles. Same per-element accumulation order and epilogue in both.
+template <int CFG>
+struct G8Geom {
+  static constexpr int BM = CFG == 0 ? 256 : 128, BN = CFG == 0 ? 256 : 384;
+  static constexpr int WM = BM / 2, WN = BN / 4;  // wave tile (2 x 4 waves)
+  static constexpr int HM = WM / 2, HN = WN / 2;  // one phase's quadrant
+  static constexpr int NI = HM / 16, NJ = HN / 16;
+  static constexpr int SA = BM / 2 * 128, SB = BN / 2 * 128;  // A / B half-tile slot bytes
+  static constexpr int PA = BM / 128, PB = BN / 128;          // 1 KiB LDS-DMA pieces per wave per slot
+  static constexpr int slot_off(int sl) { return sl == 0 ? 0 : sl == 1 ? SA : sl == 2 ? SA + SB : SA + 2 * SB; }
+  static constexpr int pieces(int sl) { return (sl == 0 || sl == 3) ? PA : PB; }
+  static_assert(2 * SA + 2 * SB == G8_BUF, "a K-tile is 64 KiB");
+  static_assert(NJ == 2 || NJ == 3, "column permutation below");
+};
+// tile column (within a wave-column half) of B LDS row jj: lane group f of the 16 x 16 MFMA
+// blocks owns consecutive columns — 8 for the block pair jb = 0, 1 (one 16-byte f16 store),
+// 4 for a third block jb = 2 (one 8-byte store)
+__device__ __forceinline__ int g8_colperm(int jj) {
+  const int jb = jj >> 4, f = (jj >> 2) & 3, r = jj & 3;
+  return jb < 2 ? 8 * f + 4 * jb + r : 32 + 4 * f + r;
+}
 
 #define MRAG_VMCNT_CASE(n) \
   case n: asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory"); break;
-__device__ __forceinline__ void vmcnt_wait(int n) {  // n wave-uniform, even, 0..42
+__device__ __forceinline__ void vmcnt_wait(int n) {  // n wave-uniform, 0..63
   switch (n) {
-    MRAG_VMCNT_CASE(2) MRAG_VMCNT_CASE(4) MRAG_VMCNT_CASE(6) MRAG_VMCNT_CASE(8) MRAG_VMCNT_CASE(10)
-    MRAG_VMCNT_CASE(12) MRAG_VMCNT_CASE(14) MRAG_VMCNT_CASE(16) MRAG_VMCNT_CASE(18) MRAG_VMCNT_CASE(20)
-    MRAG_VMCNT_CASE(22) MRAG_VMCNT_CASE(24) MRAG_VMCNT_CASE(26) MRAG_VMCNT_CASE(28) MRAG_VMCNT_CASE(30)
-    MRAG_VMCNT_CASE(32) MRAG_VMCNT_CASE(34) MRAG_VMCNT_CASE(36) MRAG_VMCNT_CASE(38) MRAG_VMCNT_CASE(40)
-    MRAG_VMCNT_CASE(42)
+    MRAG_VMCNT_CASE(1) MRAG_VMCNT_CASE(2) MRAG_VMCNT_CASE(3) MRAG_VMCNT_CASE(4) MRAG_VMCNT_CASE(5)
+    MRAG_VMCNT_CASE(6) MRAG_VMCNT_CASE(7) MRAG_VMCNT_CASE(8) MRAG_VMCNT_CASE(9) MRAG_VMCNT_CASE(10)
+    MRAG_VMCNT_CASE(11) MRAG_VMCNT_CASE(12) MRAG_VMCNT_CASE(13) MRAG_VMCNT_CASE(14) MRAG_VMCNT_CASE(15)
+    MRAG_VMCNT_CASE(16) MRAG_VMCNT_CASE(17) MRAG_VMCNT_CASE(18) MRAG_VMCNT_CASE(19) MRAG_VMCNT_CASE(20)
+    MRAG_VMCNT_CASE(21) MRAG_VMCNT_CASE(22) MRAG_VMCNT_CASE(23) MRAG_VMCNT_CASE(24) MRAG_VMCNT_CASE(25)
+    MRAG_VMCNT_CASE(26) MRAG_VMCNT_CASE(27) MRAG_VMCNT_CASE(28) MRAG_VMCNT_CASE(29) MRAG_VMCNT_CASE(30)
+    MRAG_VMCNT_CASE(31) MRAG_VMCNT_CASE(32) MRAG_VMCNT_CASE(33) MRAG_VMCNT_CASE(34) MRAG_VMCNT_CASE(35)
+    MRAG_VMCNT_CASE(36) MRAG_VMCNT_CASE(37) MRAG_VMCNT_CASE(38) MRAG_VMCNT_CASE(39) MRAG_VMCNT_CASE(40)
+    MRAG_VMCNT_CASE(41) MRAG_VMCNT_CASE(42) MRAG_VMCNT_CASE(43) MRAG_VMCNT_CASE(44) MRAG_VMCNT_CASE(45)
+    MRAG_VMCNT_CASE(46) MRAG_VMCNT_CASE(47) MRAG_VMCNT_CASE(48) MRAG_VMCNT_CASE(49) MRAG_VMCNT_CASE(50)
+    MRAG_VMCNT_CASE(51) MRAG_VMCNT_CASE(52) MRAG_VMCNT_CASE(53) MRAG_VMCNT_CASE(54) MRAG_VMCNT_CASE(55)
+    MRAG_VMCNT_CASE(56) MRAG_VMCNT_CASE(57) MRAG_VMCNT_CASE(58) MRAG_VMCNT_CASE(59) MRAG_VMCNT_CASE(60)
+    MRAG_VMCNT_CASE(61) MRAG_VMCNT_CASE(62) MRAG_VMCNT_CASE(63)
     default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
   }
 }
@@ -268,10 +300,13 @@ __device__ __forceinline__ void vmcnt_wait(int n) {  // n wave-uniform, even, 0.
 // ABL (timing experiments only, wrong results): 1 = no LDS-DMA in the loop, 2 = no
 // fragment ds_reads in the loop, 3 = both, 4 = no ping-pong stagger, 5 = LDS-DMA from the
 // first two K-tiles only (L2-hot), 7 = no epilogue stores
-template <int EPI, int ABL = 0>
+template <int EPI, int ABL = 0, int CFG = 0>
 __global__ __launch_bounds__(G8_THREADS) void gemm_8p_kernel(GemmArgs g) {
-  __shared__ __attribute__((aligned(16))) char smem[8 * G8_SLOT + (ABL == 8 ? 16 : G8_BIAS_MAX * 4)];
-  float* sbias = (float*)(smem + 8 * G8_SLOT);
+  using GG = G8Geom<CFG>;
+  constexpr int BM = GG::BM, BN = GG::BN, WM = GG::WM, WN = GG::WN, HM = GG::HM, HN = GG::HN;
+  constexpr int NI = GG::NI, NJ = GG::NJ, PA = GG::PA, PB = GG::PB;
+  __shared__ __attribute__((aligned(16))) char smem[2 * G8_BUF + (ABL == 8 ? 16 : G8_BIAS_MAX * 4)];
+  float* sbias = (float*)(smem + 2 * G8_BUF);
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wr = w >> 2, wc = w & 3;
@@ -279,8 +314,8 @@ __global__ __launch_bounds__(G8_THREADS) void gemm_8p_kernel(GemmArgs g) {
   const uint32_t lds_base = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)((AS3 char*)smem));
 
   // this workgroup's tiles: lo + s + k * nbx, k = 0 .. my_n - 1
-  const int tiles_n = g.N / G8_BN;
-  const int ntiles = ((g.M + G8_BM - 1) / G8_BM) * tiles_n;
+  const int tiles_n = g.N / BN;
+  const int ntiles = ((g.M + BM - 1) / BM) * tiles_n;
   const int xcd = blockIdx.x & 7, sidx = blockIdx.x >> 3;
   const int nbx = ((int)gridDim.x - xcd + 7) >> 3;
   const int q8 = ntiles >> 3, r8 = ntiles & 7;
@@ -298,51 +333,56 @@ __global__ __launch_bounds__(G8_THREADS) void gemm_8p_kernel(GemmArgs g) {
   const int KH = 4 * ktiles;       // half-tiles per tile
   const int total = my_n * KH;     // half-tiles of the whole stream
 
-  // staging: this wave fills pieces 2w, 2w + 1 (8 LDS rows each) of every slot; LDS row
-  // j = 16 w + 8 q + (lane >> 3), chunk position lane & 7 holds source chunk
-  // (lane & 7) ^ ((j >> 1) & 7)
-  int rowA[2][2], colB[2][2], coffq[2];
+  // staging: a slot with PX pieces per wave gets pieces PX w .. PX w + PX - 1 (8 LDS rows each)
+  // from this wave; LDS row j = 8 (PX w + q) + (lane >> 3), chunk position lane & 7 holds
+  // source chunk (lane & 7) ^ ((j >> 1) & 7).
+  // A slot h: LDS row j holds tile row WM (j / HM) + HM h + j % HM (wave-row j / HM, half h).
+  // B slot h: LDS row j = HN wc + 16 jb + 4 f + r holds tile column WN wc + HN h + g8_colperm(j % HN).
+  int rowA[2][PA], colB[2][PB], coffA[PA], coffB[PB];
 #pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    const int j = 16 * w + 8 * q + (lane >> 3);
-    coffq[q] = ((lane & 7) ^ ((j >> 1) & 7)) * 8;
+  for (int q = 0; q < PA; ++q) {
+    const int j = 8 * (PA * w + q) + (lane >> 3);
+    coffA[q] = ((lane & 7) ^ ((j >> 1) & 7)) * 8;
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      rowA[h][q] = (j & 63) + 128 * (j >> 6) + 64 * h;
-      // LDS row 32 wc + 16 jb + 4 f + r (f, r < 4) holds tile column 64 wc + 32 h + 8 f + 4 jb + r,
-      // so lane group f of a 16x16 block pair (jb = 0, 1) owns 8 consecutive columns
-      const int jj = j & 31;
-      colB[h][q] = 64 * (j >> 5) + 32 * h + 8 * ((jj >> 2) & 3) + 4 * (jj >> 4) + (jj & 3);
-    }
+    for (int h = 0; h < 2; ++h) rowA[h][q] = WM * (j / HM) + HM * h + j % HM;
+  }
+#pragma unroll
+  for (int q = 0; q < PB; ++q) {
+    const int j = 8 * (PB * w + q) + (lane >> 3);
+    coffB[q] = ((lane & 7) ^ ((j >> 1) & 7)) * 8;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) colB[h][q] = WN * (j / HN) + HN * h + g8_colperm(j % HN);
   }
   // The stream is consumed strictly in order (prologue L[0..6], then L[phi + 7]); phase p of
   // a K-tile always issues slot (p + 3) & 3, a compile-time constant, so the loader keeps
   // its K-tile position incrementally and recomputes this lane's source-row element
   // offsets once per tile (no per-phase division or slot selection).
   int ld_kt = 0, ld_par = 0, ld_T = lo + sidx;
-  int gA[2][2], gB[2][2];  // element offsets (row * ld + chunk) for the tile being loaded
+  int gA[2][PA], gB[2][PB];  // element offsets (row * ld + chunk) for the tile being loaded
   auto load_tile_offsets = [&]() {
     const int tm = ld_T / tiles_n;
-    const int m0 = tm * G8_BM, n0 = (ld_T - tm * tiles_n) * G8_BN;
+    const int m0 = tm * BM, n0 = (ld_T - tm * tiles_n) * BN;
 #pragma unroll
-    for (int q = 0; q < 2; ++q)
+    for (int h = 0; h < 2; ++h) {
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        gA[h][q] = min(m0 + rowA[h][q], g.M - 1) * g.lda + coffq[q];
-        gB[h][q] = (n0 + colB[h][q]) * g.ldw + coffq[q];
-      }
+      for (int q = 0; q < PA; ++q) gA[h][q] = min(m0 + rowA[h][q], g.M - 1) * g.lda + coffA[q];
+#pragma unroll
+      for (int q = 0; q < PB; ++q) gB[h][q] = (n0 + colB[h][q]) * g.ldw + coffB[q];
+    }
   };
   load_tile_offsets();
   auto stage_slot = [&](auto SL) {
     constexpr int sl = decltype(SL)::value;
+    constexpr int PX = GG::pieces(sl);
     const int k0 = (ABL == 5 ? (ld_kt & 1) : ld_kt) * GK;
-    const uint32_t dst = lds_base + (uint32_t)((ld_par * 4 + sl) * G8_SLOT) + (uint32_t)(w * 2048);
+    const uint32_t dst = lds_base + (uint32_t)(ld_par * G8_BUF + GG::slot_off(sl)) + (uint32_t)(w * PX * 1024);
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const _Float16* src = (sl == 0)   ? g.A + gA[0][q]
-                            : (sl == 1) ? g.W + gB[0][q]
-                            : (sl == 2) ? g.W + gB[1][q]
-                                        : g.A + gA[1][q];
+    for (int q = 0; q < PX; ++q) {
+      const _Float16* src;
+      if constexpr (sl == 0) src = g.A + gA[0][q];
+      else if constexpr (sl == 1) src = g.W + gB[0][q];
+      else if constexpr (sl == 2) src = g.W + gB[1][q];
+      else src = g.A + gA[1][q];
       glds_x4(src + k0, dst + q * 1024);
     }
     if constexpr (sl == 3) {  // K-tile complete: advance the loader
@@ -359,43 +399,43 @@ __global__ __launch_bounds__(G8_THREADS) void gemm_8p_kernel(GemmArgs g) {
   using S2 = std::integral_constant<int, 2>;
   using S3 = std::integral_constant<int, 3>;
 
-  int offA[4][2], offB[2][2];
+  int offA[NI][2], offB[NJ][2];
 #pragma unroll
   for (int kk = 0; kk < 2; ++kk) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) offA[i][kk] = swz_off(64 * wr + 16 * i + fr, kk * 4 + fq);
+    for (int i = 0; i < NI; ++i) offA[i][kk] = swz_off(HM * wr + 16 * i + fr, kk * 4 + fq);
 #pragma unroll
-    for (int jb = 0; jb < 2; ++jb) offB[jb][kk] = swz_off(32 * wc + 16 * jb + fr, kk * 4 + fq);
+    for (int jb = 0; jb < NJ; ++jb) offB[jb][kk] = swz_off(HN * wc + 16 * jb + fr, kk * 4 + fq);
   }
 
-  f32x4 acc[2][2][4][2];  // [h][hh][i][jb]
-  half8 fa[4][2], fb0[2][2], fb1[2][2];
+  f32x4 acc[2][2][NI][NJ];  // [h][hh][i][jb]
+  half8 fa[NI][2], fb0[NJ][2], fb1[NJ][2];
   auto readA = [&](const char* slot) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < NI; ++i)
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
         if constexpr (ABL == 2 || ABL == 3) asm volatile("" : "+v"(fa[i][kk]));
         else fa[i][kk] = *(const half8*)(slot + offA[i][kk]);
       }
   };
-  auto readB = [&](const char* slot, half8 (&fb)[2][2]) {
+  auto readB = [&](const char* slot, half8 (&fb)[NJ][2]) {
 #pragma unroll
-    for (int jb = 0; jb < 2; ++jb)
+    for (int jb = 0; jb < NJ; ++jb)
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
         if constexpr (ABL == 2 || ABL == 3) asm volatile("" : "+v"(fb[jb][kk]));
         else fb[jb][kk] = *(const half8*)(slot + offB[jb][kk]);
       }
   };
-  auto mfma_q = [&](f32x4 (&a)[4][2], const half8 (&fb)[2][2]) {
+  auto mfma_q = [&](f32x4 (&a)[NI][NJ], const half8 (&fb)[NJ][2]) {
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < NI; ++i)
 #pragma unroll
-        for (int jb = 0; jb < 2; ++jb)
+        for (int jb = 0; jb < NJ; ++jb)
           a[i][jb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fb[jb][kk], fa[i][kk], a[i][jb], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
   };
@@ -408,18 +448,25 @@ __global__ __launch_bounds__(G8_THREADS) void gemm_8p_kernel(GemmArgs g) {
   int st_cnt = 0;     // vector stores that epilogue issued (wave-uniform)
   // end of a read segment: issue L[phi + 7] (slot SL), wait for L[phi + 2] (read by phase
   // phi + 1) and for this segment's own ds_reads, barrier
+  // LDS-DMA instructions of L[i + 1 .. last] (the stream's slot i & 3 has pieces(i & 3) each)
+  auto younger = [&](int i, int last) {
+    int n = 0;
+    for (int t = i + 1; t <= last; ++t) n += ((t & 3) == 0 || (t & 3) == 3) ? PA : PB;
+    return n;
+  };
   auto end_reads = [&](int phi, auto SL) {
+    constexpr int sl = decltype(SL)::value;
+    // steady state: L[phi + 3 .. phi + 7] in flight = every slot once + slot sl again
+    constexpr int YSTEADY = 2 * PA + 2 * PB + GG::pieces(sl);
     const bool full = phi + 7 < total;  // five younger half-tiles in flight
     if (ABL != 1 && ABL != 3 && full) stage_slot(SL);
     const bool post = phi - st_phi <= 5;  // the last epilogue's stores are younger than L[phi + 2]
     if (__builtin_expect(full && !post, 1)) {
-      asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
-    } else if (full && st_cnt == 32) {
-      asm volatile("s_waitcnt vmcnt(42)" ::: "memory");
-    } else if (full && st_cnt == 16) {
-      asm volatile("s_waitcnt vmcnt(26)" ::: "memory");
+      vmcnt_wait(YSTEADY);
+    } else if (full) {
+      vmcnt_wait(YSTEADY + st_cnt);
     } else {
-      vmcnt_wait(2 * min(5, max(0, total - 1 - (phi + 2))) + (post ? st_cnt : 0));
+      vmcnt_wait(younger(phi + 2, total - 1) + (post ? st_cnt : 0));
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     bar();
@@ -434,7 +481,7 @@ __global__ __launch_bounds__(G8_THREADS) void gemm_8p_kernel(GemmArgs g) {
     if (last >= 4) stage_slot(S0{});
     if (last >= 5) stage_slot(S1{});
     if (last >= 6) stage_slot(S2{});
-    vmcnt_wait(2 * min(5, max(0, total - 2)));
+    vmcnt_wait(younger(1, last));  // L[0], L[1] landed
     bar();
   }
   // waves 4..7 (one per SIMD beside a wave of 0..3) run one barrier behind waves 0..3
@@ -446,21 +493,21 @@ __global__ __launch_bounds__(G8_THREADS) void gemm_8p_kernel(GemmArgs g) {
 #pragma unroll
       for (int hh = 0; hh < 2; ++hh)
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < NI; ++i)
 #pragma unroll
-          for (int jb = 0; jb < 2; ++jb) acc[h][hh][i][jb] = f32x4{};
+          for (int jb = 0; jb < NJ; ++jb) acc[h][hh][i][jb] = f32x4{};
     for (int kt = 0; kt < ktiles; ++kt, phi += 4) {
-      const char* buf = (const char*)smem + ((phi >> 2) & 1) * 4 * G8_SLOT;
-      readA(buf + 0 * G8_SLOT);  // phase 0: (h0, hh0)
-      readB(buf + 1 * G8_SLOT, fb0);
+      const char* buf = (const char*)smem + ((phi >> 2) & 1) * G8_BUF;
+      readA(buf + GG::slot_off(0));  // phase 0: (h0, hh0)
+      readB(buf + GG::slot_off(1), fb0);
       end_reads(phi, S3{});
       mfma_q(acc[0][0], fb0);
       bar();
-      readB(buf + 2 * G8_SLOT, fb1);  // phase 1: (h0, hh1)
+      readB(buf + GG::slot_off(2), fb1);  // phase 1: (h0, hh1)
       end_reads(phi + 1, S0{});
       mfma_q(acc[0][1], fb1);
       bar();
-      readA(buf + 3 * G8_SLOT);  // phase 2: (h1, hh1)
+      readA(buf + GG::slot_off(3));  // phase 2: (h1, hh1)
       end_reads(phi + 2, S1{});
       mfma_q(acc[1][1], fb1);
       bar();
@@ -471,23 +518,29 @@ __global__ __launch_bounds__(G8_THREADS) void gemm_8p_kernel(GemmArgs g) {
     st_phi = phi - 1;
     st_cnt = 0;
 
-    // epilogue: blocks (h, hh, i, jb = 0, 1): row 128 wr + 64 h + 16 i + fr, columns
-    // 64 wc + 32 hh + 8 fq + 4 jb + (0..3): one 16-byte f16 store (two for f32) per lane
+    // epilogue: blocks (h, hh, i): row WM wr + HM h + 16 i + fr; columns WN wc + HN hh + 8 fq
+    // + (0..7) from the block pair jb = 0, 1 (one 16-byte f16 store, two for f32) and, for
+    // CFG 1, WN wc + HN hh + 32 + 4 fq + (0..3) from jb = 2 (one 8-byte f16 / 16-byte f32 store)
     const int T = lo + sidx + tl * nbx;
     const int tm = T / tiles_n;
-    const int m0 = tm * G8_BM, n0 = (T - tm * tiles_n) * G8_BN;
-    constexpr int SPB = (EPI == EPI_F32_RESIDUAL || EPI == EPI_F32) ? 2 : 1;  // stores per block
+    const int m0 = tm * BM, n0 = (T - tm * tiles_n) * BN;
+    constexpr int SPB = ((EPI == EPI_F32_RESIDUAL || EPI == EPI_F32) ? 2 : 1) + (NJ == 3 ? 1 : 0);
 #pragma unroll
     for (int hh = 0; hh < 2; ++hh) {
-      const int n = n0 + 64 * wc + 32 * hh + 8 * fq;
-      float bn[8];
+      const int nb = n0 + WN * wc + HN * hh;
+      const int n = nb + 8 * fq;
+      float bn[8], bn4[4];
 #pragma unroll
       for (int r = 0; r < 8; ++r) bn[r] = ABL == 8 ? 0.f : sbias[n + r];
+      if constexpr (NJ == 3) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bn4[r] = ABL == 8 ? 0.f : sbias[nb + 32 + 4 * fq + r];
+      }
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int mb = m0 + 128 * wr + 64 * h + 16 * i;  // wave-uniform block row
+        for (int i = 0; i < NI; ++i) {
+          const int mb = m0 + WM * wr + HM * h + 16 * i;  // wave-uniform block row
           const int m = mb + fr;
           if constexpr (ABL == 7) {
             asm volatile("" ::"v"(acc[h][hh][i][0]), "v"(acc[h][hh][i][1]), "v"(bn[0]));
@@ -495,6 +548,7 @@ __global__ __launch_bounds__(G8_THREADS) void gemm_8p_kernel(GemmArgs g) {
             st_cnt += SPB;        // SPB vector stores (counted for the vmcnt bookkeeping)
             if (m < g.M) {
               gemm_store8<EPI>(g, m, n, acc[h][hh][i][0], acc[h][hh][i][1], bn);
+              if constexpr (NJ == 3) gemm_store4<EPI>(g, m, nb + 32 + 4 * fq, acc[h][hh][i][NJ - 1], bn4);
             }
           }
         }
@@ -1120,8 +1174,24 @@ int num_cus() {
   return n;
 }
 
-int launch_gemm_8p(const GemmArgs& g, int epi, hipStream_t s) {
-  const int ntiles = ((g.M + G8_BM - 1) / G8_BM) * (g.N / G8_BN);
+// K3d geometry: CFG 0 (256 x 256) unless env MRAG_G8_CFG=1 asks for CFG 1 (128 x 384) where
+// N % 384 == 0. CFG 1 fills 200 instead of 150 CUs at N = 768 but measured no faster (fc2
+// 97-99 us, out-proj 44 us either way; qkv 78 vs 59 us: notes/gemm_experiments.md), so the
+// persistent 256 x 256 kernel stays the default; CFG 1 is kept for A/B timing and is covered by
+// the parity tests (env-forced).
+int g8_pick_cfg(const GemmArgs& g) {
+  static const int force = [] {
+    const char* e = getenv("MRAG_G8_CFG");
+    return e ? atoi(e) : -1;
+  }();
+  if (force == 1 && g.N % 384 == 0) return 1;
+  return g.N % 256 == 0 ? 0 : -1;
+}
+
+template <int CFG>
+int launch_gemm_8p_cfg(const GemmArgs& g, int epi, hipStream_t s) {
+  using GG = G8Geom<CFG>;
+  const int ntiles = ((g.M + GG::BM - 1) / GG::BM) * (g.N / GG::BN);
   int nb = std::min((ntiles + 7) / 8 * 8, std::max(8, num_cus() / 8 * 8));
   static const int grid_override = [] {
     const char* e = getenv("MRAG_G8_GRID");
@@ -1130,7 +1200,7 @@ int launch_gemm_8p(const GemmArgs& g, int epi, hipStream_t s) {
   if (grid_override > 0) nb = std::min(nb, grid_override);
   static bool said = false;
   if (!said && getenv("MRAG_G8_VERBOSE")) {
-    fprintf(stderr, "K3d: %d CUs, grid %d for %d tiles\n", num_cus(), nb, ntiles);
+    fprintf(stderr, "K3d cfg %d: %d CUs, grid %d for %d tiles\n", CFG, num_cus(), nb, ntiles);
     said = true;
   }
   const dim3 grid((unsigned)nb);
@@ -1138,7 +1208,7 @@ int launch_gemm_8p(const GemmArgs& g, int epi, hipStream_t s) {
     const char* e = getenv("MRAG_GEMM_ABL");
     return e ? atoi(e) : 0;
   }();
-  if (abl != 0 && epi == EPI_F16) {
+  if (CFG == 0 && abl != 0 && epi == EPI_F16) {
     switch (abl) {
       case 1: hipLaunchKernelGGL((gemm_8p_kernel<EPI_F16, 1>), grid, dim3(G8_THREADS), 0, s, g); break;
       case 2: hipLaunchKernelGGL((gemm_8p_kernel<EPI_F16, 2>), grid, dim3(G8_THREADS), 0, s, g); break;
@@ -1152,11 +1222,17 @@ int launch_gemm_8p(const GemmArgs& g, int epi, hipStream_t s) {
     return MRAG_OK;
   }
   switch (epi) {
-    case EPI_F16: hipLaunchKernelGGL(gemm_8p_kernel<EPI_F16>, grid, dim3(G8_THREADS), 0, s, g); break;
-    case EPI_F16_QUICK_GELU: hipLaunchKernelGGL(gemm_8p_kernel<EPI_F16_QUICK_GELU>, grid, dim3(G8_THREADS), 0, s, g); break;
-    case EPI_F16_GELU_ERF: hipLaunchKernelGGL(gemm_8p_kernel<EPI_F16_GELU_ERF>, grid, dim3(G8_THREADS), 0, s, g); break;
-    case EPI_F32_RESIDUAL: hipLaunchKernelGGL(gemm_8p_kernel<EPI_F32_RESIDUAL>, grid, dim3(G8_THREADS), 0, s, g); break;
-    case EPI_F32: hipLaunchKernelGGL(gemm_8p_kernel<EPI_F32>, grid, dim3(G8_THREADS), 0, s, g); break;
+    case EPI_F16: hipLaunchKernelGGL((gemm_8p_kernel<EPI_F16, 0, CFG>), grid, dim3(G8_THREADS), 0, s, g); break;
+    case EPI_F16_QUICK_GELU:
+      hipLaunchKernelGGL((gemm_8p_kernel<EPI_F16_QUICK_GELU, 0, CFG>), grid, dim3(G8_THREADS), 0, s, g);
+      break;
+    case EPI_F16_GELU_ERF:
+      hipLaunchKernelGGL((gemm_8p_kernel<EPI_F16_GELU_ERF, 0, CFG>), grid, dim3(G8_THREADS), 0, s, g);
+      break;
+    case EPI_F32_RESIDUAL:
+      hipLaunchKernelGGL((gemm_8p_kernel<EPI_F32_RESIDUAL, 0, CFG>), grid, dim3(G8_THREADS), 0, s, g);
+      break;
+    case EPI_F32: hipLaunchKernelGGL((gemm_8p_kernel<EPI_F32, 0, CFG>), grid, dim3(G8_THREADS), 0, s, g); break;
     default: return mrag::fail(MRAG_ERR_ARG, "gemm: bad epilogue %d", epi);
   }
   MRAG_CHECK_LAUNCH();
@@ -1168,7 +1244,11 @@ int launch_gemm(const GemmArgs& g, int epi, hipStream_t s) {
   MRAG_REQUIRE(g.N % GN == 0 && g.K % GK == 0, "gemm: N=%d must be a multiple of %d and K=%d of %d", g.N, GN, g.K,
                GK);
   MRAG_REQUIRE(g.lda % 8 == 0 && g.ldw % 8 == 0 && g.ldc % 4 == 0, "gemm: lda/ldw must be multiples of 8, ldc of 4");
-  if (gemm_big_mode() != 0 && g.M >= 1024 && g.N % G8_BN == 0 && g.N <= G8_BIAS_MAX) return launch_gemm_8p(g, epi, s);
+  if (gemm_big_mode() != 0 && g.M >= 1024 && g.N <= G8_BIAS_MAX) {
+    const int cfg = g8_pick_cfg(g);
+    if (cfg == 0) return launch_gemm_8p_cfg<0>(g, epi, s);
+    if (cfg == 1) return launch_gemm_8p_cfg<1>(g, epi, s);
+  }
   const dim3 grid((unsigned)(((g.M + GM - 1) / GM) * (g.N / GN)));
   switch (epi) {
     case EPI_F16: hipLaunchKernelGGL(gemm_nt_kernel<EPI_F16>, grid, dim3(GTHREADS), 0, s, g); break;

@@ -1867,7 +1867,11 @@ int mrag_knn_search(mrag_knn_index* ix, const float* queries, int64_t nq, int32_
     const dim3 sgrid((unsigned)(qgroups * S));
     // Sample pre-pass (v2 only, when every split has >= 64 tiles): seeds the shared
     // threshold near the k-th best so the main scan's list insertions stay rare.
-    const int sample_stride = 16;
+    static const int sample_stride = [] {  // env MRAG_SAMPLE_STRIDE (A/B timing); default 16
+      const char* e = getenv("MRAG_SAMPLE_STRIDE");
+      const int v = e ? atoi(e) : 16;
+      return v >= 2 ? v : 16;
+    }();
     const int min_tiles = ntiles / S;
     if (use_v2 && !ix->no_sample && min_tiles >= 4 * sample_stride) {
       sp.sample_stride = sample_stride;

@@ -65,7 +65,8 @@ def test_gemm_epilogues(cuda, epi):
     assert err < 1e-2, err
 
 
-@pytest.mark.parametrize("M,N,K", [(1100, 768, 768), (2048, 384, 320), (1024, 2304, 192), (8300, 2304, 128)])
+@pytest.mark.parametrize("M,N,K", [(1100, 768, 768), (2048, 384, 320), (1024, 2304, 192), (8300, 2304, 128),
+                                   (2100, 1536, 256), (12800, 768, 3072)])
 @pytest.mark.parametrize("epi", [0, 1, 2, 3, 4])
 def test_gemm_big_tiles(cuda, M, N, K, epi):
     """K3d (persistent 256 x 256 tiles, used from M = 1024 when N % 256 == 0; K3 otherwise):
@@ -154,3 +155,41 @@ def test_minilm_max_length_256(cuda):
     mask[1, 200:] = 0
     enc = GpuEncoder(MINILM_L6)
     _cmp(enc.embed_tokens(ids, mask), minilm_embeds(bert_model(0), ids, mask))
+
+
+def test_gemm_cfg1_128x384_forced(cuda):
+    """K3d CFG 1 (128 x 384 tiles, opt-in via MRAG_G8_CFG=1, read once per process): every
+    epilogue on ragged M and N = 768 / 1536, in a child process with the variable set."""
+    import subprocess
+    import sys
+
+    code = r'''
+import sys, torch
+sys.path[:0] = [sys.argv[1], sys.argv[2]]
+from app.encoders import gemm_nt
+for (M, N, K) in [(1100, 768, 768), (2100, 1536, 256), (12800, 768, 3072)]:
+    for epi in range(5):
+        g = torch.Generator(device="cuda").manual_seed(epi)
+        A = (torch.randn(M, K, generator=g, device="cuda") * 0.5).half()
+        W = (torch.randn(N, K, generator=g, device="cuda") * 0.05).half()
+        bias = torch.randn(N, generator=g, device="cuda") * 0.1
+        ref = A.float() @ W.float().t() + bias
+        if epi == 1: ref = ref * torch.sigmoid(1.702 * ref)
+        elif epi == 2: ref = torch.nn.functional.gelu(ref)
+        if epi <= 2: C = torch.full((M, N), float("nan"), dtype=torch.float16, device="cuda")
+        elif epi == 3:
+            C0 = torch.randn(M, N, generator=g, device="cuda"); C = C0.clone(); ref = ref + C0
+        else: C = torch.full((M, N), float("nan"), dtype=torch.float32, device="cuda")
+        gemm_nt(A, W, bias, C, epi)
+        torch.cuda.synchronize()
+        assert not torch.isnan(C.float()).any(), (M, N, K, epi)
+        err = (C.float() - ref).abs().max().item() / ref.abs().max().item()
+        assert err < 1e-2, (M, N, K, epi, err)
+print("ok")
+'''
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, MRAG_G8_CFG="1", MRAG_G8_VERBOSE="1")
+    res = subprocess.run([sys.executable, "-c", code, os.path.join(root, "multimodal-rag-for-image-text-search_amd"),
+                          root], env=env, capture_output=True, text=True, timeout=240)
+    assert res.returncode == 0 and "ok" in res.stdout, res.stderr[-2000:]
+    assert "K3d cfg 1" in res.stderr
