@@ -870,7 +870,7 @@ __global__ __launch_bounds__(256) void attention_mfma64_kernel(AttentionArgs a) 
     }
 }
 
-// K4 v2 (MFMA form, L <= 64, head_dim 64): as v1 up to the softmax, then
+// K4 v2 (MFMA form, L <= 64, head_dim 64 or 32): as v1 up to the softmax, then
 //   O^T = V^T . P^T: P^T is the S^T accumulator itself (registers 8t..8t+7 of key block kb
 //                   are the B fragment of k-step 2kb + t, key order permuted: element j <->
 //                   key 16s + 8(j>>2) + 4h + (j&3)); the V^T A fragments come from the row-major
@@ -888,9 +888,12 @@ __device__ __forceinline__ half4_t lds_read_tr16(const _Float16* p) {
   return __builtin_bit_cast(half4_t, v);
 }
 
+template <int DH>  // 64 (CLIP) or 32 (MiniLM)
 __global__ __launch_bounds__(256) void attention_mfma64t_kernel(AttentionArgs a) {
-  constexpr int DH = 64;
-  constexpr int VROW = 96;  // 192-byte rows: the 4 rows of one transposed read hit disjoint banks
+  constexpr int KS = DH / 16;  // 16-dim k-steps of S^T = K . Q^T
+  constexpr int DB = DH / 32;  // 32-dim output blocks of O^T
+  constexpr int LPR = DH / 8;  // lanes per V row (16 B each)
+  constexpr int VROW = 96;     // 192-byte rows: the 4 rows of one transposed read hit disjoint banks
   __shared__ __attribute__((aligned(16))) _Float16 Vs[4][64 * VROW];
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
@@ -905,14 +908,14 @@ __global__ __launch_bounds__(256) void attention_mfma64t_kernel(AttentionArgs a)
 
   // V rows -> LDS: 8 lanes x 16 B per row, 8 rows per instruction, zero rows >= L
 #pragma unroll
-  for (int it = 0; it < 8; ++it) {
-    const int key = 8 * it + (lane >> 3), c = lane & 7;
+  for (int it = 0; it < LPR; ++it) {  // LPR lanes x 16 B per row, 64 / LPR rows per instruction
+    const int key = (64 / LPR) * it + lane / LPR, c = lane % LPR;
     half8 v = {};
     if (key < L) v = *(const half8*)(base + (size_t)key * rs + 2 * D + hd * DH + 8 * c);
     *(half8*)(vs + key * VROW + 8 * c) = v;
   }
   // K (A operand) and Q (B operand) fragments: row r + 32*blk, dims 16s + 8hh .. +7
-  half8 kf[2][4], qf[2][4];
+  half8 kf[2][KS], qf[2][KS];
 #pragma unroll
   for (int blk = 0; blk < 2; ++blk) {
     const int row = r + 32 * blk;
@@ -920,7 +923,7 @@ __global__ __launch_bounds__(256) void attention_mfma64t_kernel(AttentionArgs a)
     const _Float16* kr = base + (size_t)row * rs + D + hd * DH + 8 * hh;
     const _Float16* qr = base + (size_t)row * rs + hd * DH + 8 * hh;
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
+    for (int s = 0; s < KS; ++s) {
       kf[blk][s] = ok ? *(const half8*)(kr + 16 * s) : half8{};
       qf[blk][s] = ok ? *(const half8*)(qr + 16 * s) : half8{};
     }
@@ -932,7 +935,7 @@ __global__ __launch_bounds__(256) void attention_mfma64t_kernel(AttentionArgs a)
     for (int qb = 0; qb < 2; ++qb) {
       f32x16 acc = {};
 #pragma unroll
-      for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf[kb][s], qf[qb][s], acc, 0, 0, 0);
+      for (int s = 0; s < KS; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf[kb][s], qf[qb][s], acc, 0, 0, 0);
       st[kb][qb] = acc;
     }
   // softmax over keys for the lane's two queries (as v1); P^T fragments in permuted key order
@@ -977,9 +980,9 @@ __global__ __launch_bounds__(256) void attention_mfma64t_kernel(AttentionArgs a)
   // V^T fragments: 16-lane group g reads rows (keys) r0 .. r0 + 3, columns (dims) c0 + 4p .. + 3
   // (lane 4q + p of the group supplies row q); lane i of the group receives dim c0 + i
   const int g = lane >> 4, q4 = (lane & 15) >> 2, p4 = lane & 3;
-  half8 vf[2][4];  // [dim block][k-step]
+  half8 vf[DB][4];  // [dim block][k-step]
 #pragma unroll
-  for (int db = 0; db < 2; ++db)
+  for (int db = 0; db < DB; ++db)
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       const _Float16* pa = vs + (16 * s + 4 * hh + q4) * VROW + 32 * db + 16 * (g & 1) + 4 * p4;
@@ -991,7 +994,7 @@ __global__ __launch_bounds__(256) void attention_mfma64t_kernel(AttentionArgs a)
   for (int qb = 0; qb < 2; ++qb) {
     const int q = r + 32 * qb;
 #pragma unroll
-    for (int db = 0; db < 2; ++db) {
+    for (int db = 0; db < DB; ++db) {
       f32x16 acc = {};
 #pragma unroll
       for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(vf[db][s], pb[qb][s], acc, 0, 0, 0);
@@ -1188,6 +1191,19 @@ int g8_pick_cfg(const GemmArgs& g) {
   return g.N % 256 == 0 ? 0 : -1;
 }
 
+// K3 (128 x 128, two workgroups per CU) vs K3d (persistent 256 x 256, one per CU) by rounds:
+// a K3 round (two tiles per CU) takes ~2/3 of a K3d round (one 4x larger tile) on the same K
+// (measured at K = 512 / 2048, N = 512: 23.7 vs 35.4 us, 53.1 vs 75.5 us), so K3 wins where the
+// 256 x 256 grid leaves CUs idle and the 128 x 128 one does not — the CLIP text tower at the
+// config-5 batch (N = 512). Both kernels accumulate every element in the same order.
+bool k3_beats_k3d(const GemmArgs& g) {
+  if (g.N % 256 != 0) return true;
+  const long cus = std::max(8, num_cus() / 8 * 8);
+  const long t256 = (long)((g.M + 255) / 256) * (g.N / 256), t128 = (long)((g.M + 127) / 128) * (g.N / 128);
+  const long r_d = (t256 + cus - 1) / cus, r_3 = (t128 + 2 * cus - 1) / (2 * cus);
+  return 2 * r_3 < 3 * r_d;  // K3 time ~ (2/3) r_3 < r_d; ties stay on K3d
+}
+
 template <int CFG>
 int launch_gemm_8p_cfg(const GemmArgs& g, int epi, hipStream_t s) {
   using GG = G8Geom<CFG>;
@@ -1244,7 +1260,7 @@ int launch_gemm(const GemmArgs& g, int epi, hipStream_t s) {
   MRAG_REQUIRE(g.N % GN == 0 && g.K % GK == 0, "gemm: N=%d must be a multiple of %d and K=%d of %d", g.N, GN, g.K,
                GK);
   MRAG_REQUIRE(g.lda % 8 == 0 && g.ldw % 8 == 0 && g.ldc % 4 == 0, "gemm: lda/ldw must be multiples of 8, ldc of 4");
-  if (gemm_big_mode() != 0 && g.M >= 1024 && g.N <= G8_BIAS_MAX) {
+  if (gemm_big_mode() != 0 && g.M >= 1024 && g.N <= G8_BIAS_MAX && !k3_beats_k3d(g)) {
     const int cfg = g8_pick_cfg(g);
     if (cfg == 0) return launch_gemm_8p_cfg<0>(g, epi, s);
     if (cfg == 1) return launch_gemm_8p_cfg<1>(g, epi, s);
@@ -1294,6 +1310,14 @@ bool force_valu_attention() {
   return v;
 }
 
+bool mfma_attention_dh32() {
+  static const bool v = [] {
+    const char* e = getenv("MRAG_ATTN_DH32");
+    return e && atoi(e) == 1;
+  }();
+  return v;
+}
+
 int launch_attention(const AttentionArgs& a, int dh, hipStream_t s) {
   if (a.B <= 0) return MRAG_OK;
   MRAG_REQUIRE(a.L >= 1 && a.L <= 512, "attention: L=%d unsupported (1..512)", a.L);
@@ -1315,7 +1339,12 @@ int launch_attention(const AttentionArgs& a, int dh, hipStream_t s) {
     return e && atoi(e) == 1;
   }();
   if (dh == 64 && a.L <= 64 && !force_valu_attention() && !attn_v1) {
-    hipLaunchKernelGGL(attention_mfma64t_kernel, dim3((unsigned)((a.B * a.H + 3) / 4)), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(attention_mfma64t_kernel<64>, dim3((unsigned)((a.B * a.H + 3) / 4)), dim3(256), 0, s, a);
+  } else if (dh == 32 && a.L <= 64 && mfma_attention_dh32()) {
+    // opt-in (MRAG_ATTN_DH32=1): the BERT towers otherwise stay on the f32 VALU kernel for every
+    // L, so a sequence's result does not depend on whether its batch pads past 64 tokens
+    // (cross-encoder predict(pair) == predict(batch)[i] to 1e-6)
+    hipLaunchKernelGGL(attention_mfma64t_kernel<32>, dim3((unsigned)((a.B * a.H + 3) / 4)), dim3(256), 0, s, a);
   } else if (dh == 64 && a.L <= 64 && !force_valu_attention()) {
     hipLaunchKernelGGL(attention_mfma64_kernel, dim3((unsigned)((a.B * a.H + 3) / 4)), dim3(256), 0, s, a);
   } else if (dh == 64) {

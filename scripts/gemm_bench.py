@@ -20,6 +20,11 @@ SHAPES = {  # name: (M, N, K, epilogue)
     "fc2": (12800, 768, 3072, 3),
     "out": (12800, 768, 768, 3),
     "sq4k": (4096, 4096, 4096, 0),
+    # CLIP text tower at the config-5 query batch (1000 x 16 tokens)
+    "t_qkv": (16000, 1536, 512, 0),
+    "t_out": (16000, 512, 512, 3),
+    "t_fc1": (16000, 2048, 512, 1),
+    "t_fc2": (16000, 512, 2048, 3),
 }
 
 

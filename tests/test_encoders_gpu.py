@@ -69,7 +69,8 @@ def test_gemm_epilogues(cuda, epi):
                                    (2100, 1536, 256), (12800, 768, 3072)])
 @pytest.mark.parametrize("epi", [0, 1, 2, 3, 4])
 def test_gemm_big_tiles(cuda, M, N, K, epi):
-    """K3d (persistent 256 x 256 tiles, used from M = 1024 when N % 256 == 0; K3 otherwise):
+    """K3d (persistent 256 x 256 tiles, from M = 1024 when N % 256 == 0 and the 256 x 256 grid
+    fills the CUs at least as well as K3 would; K3 otherwise):
     ragged M (1100 = 4 x 256 + 76, 8300), 297 tiles (> one per CU: the load stream and the
     epilogue stores run across tiles), every epilogue; same tolerance as K3."""
     import torch
