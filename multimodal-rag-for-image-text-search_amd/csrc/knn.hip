@@ -836,9 +836,6 @@ __global__ __launch_bounds__(SCAN2_THREADS) void knn_scan3_kernel(ScanParams p) 
     const unsigned c = pos ^ (row & 15);
     glds_x4(gt + row * ROW_BYTES + c * 16, lds_base + buf * TILE_BYTES + piece * 1024);
   };
-  auto stage_row = [&](const char* gw, uint32_t ldsw, int i, uint32_t lane16) {
-    glds_x4_saddr((lane16 ^ (uint32_t)(i << 4)) + (uint32_t)(i * 1024), gw, ldsw + i * 1024);
-  };
   auto stage_labels = [&](int buf, int tile) {
     if (w == 0) glds_x1(p.labels + (size_t)tile * TILE_ROWS + lane, lds_base + LBL_OFF + buf * TILE_ROWS * 4);
   };
@@ -895,6 +892,12 @@ __global__ __launch_bounds__(SCAN2_THREADS) void knn_scan3_kernel(ScanParams p) 
     int lane_t = lane, offA0 = offA0_init;
     uint32_t lane16 = lane * 16;
     asm volatile("" : "+v"(lane_t), "+v"(offA0), "+v"(lane16));
+    // DP = 512: m0 holds the piece's LDS address from gap 1 to the DMA in gap 2 (nothing the
+    // compiler emits in this loop reads m0: ds_read_b128 / MFMA / VALU / SALU only); it is saved
+    // once per tile and restored before the barrier
+    uint32_t m0_keep = 0;
+    uint32_t voff = 0;
+    if constexpr (CPR == 64 && !NO_GLDS) asm volatile("s_mov_b32 %0, m0" : "=s"(m0_keep));
     half8 a[4];
     auto read_a = [&](int kk, int rb) {
       a[rb] = *(const half8*)(tb + ((offA0 ^ ((kk & 3) << 6)) + (kk >> 2) * 256 + rb * 16 * ROW_BYTES));
@@ -916,10 +919,15 @@ __global__ __launch_bounds__(SCAN2_THREADS) void knn_scan3_kernel(ScanParams p) 
         // one job per MFMA gap
         if constexpr ((j & 3) == 3) {  // after the last MFMA of block rb: its next fragment
           if constexpr (kk + 1 < KSTEPS) read_a(kk + 1, rb);
+        } else if constexpr (j == 1) {
+          if constexpr (CPR == 64 && !NO_GLDS) {
+            voff = (lane16 ^ (uint32_t)(kk << 4)) + (uint32_t)(kk * 1024);
+            asm volatile("s_mov_b32 m0, %1" : "+v"(voff) : "s"(ldsw + kk * 1024));
+          }
         } else if constexpr (j == 2) {
           if constexpr (!NO_GLDS) {
             if constexpr (CPR == 64)
-              stage_row(gw, ldsw, kk, lane16);
+              asm volatile("global_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(gw) : "memory");
             else
               stage_piece(Y, ntile, kk, lane_t);
           }
@@ -931,6 +939,7 @@ __global__ __launch_bounds__(SCAN2_THREADS) void knn_scan3_kernel(ScanParams p) 
       });
     });
     mfma16_guard(acc[X]);
+    if constexpr (CPR == 64 && !NO_GLDS) asm volatile("s_mov_b32 m0, %0" ::"s"(m0_keep));
     if (tile_mask != ~0ull) {
       const uint64_t lm = tile_mask >> (4 * g4);
 #pragma unroll
