@@ -8,3 +8,4 @@ cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_stats -o run -- python3 $R/bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-fusion > $R/gpurun_out/prof_stats.log 2>&1 || exit 3
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $R/gpurun_out/prof_fetch -o run -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-clip --no-fusion > $R/gpurun_out/prof_fetch.log 2>&1 || exit 4
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $R/gpurun_out/prof_write -o run -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-clip --no-fusion > $R/gpurun_out/prof_write.log 2>&1 || exit 5
+cd $R && timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || exit 6
