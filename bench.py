@@ -325,6 +325,20 @@ def main():
     flops_per_launch = 2.0 * NQ * ROWS_PER_GPU * DIM
     achieved_tflops = flops_per_launch / avg_scan_s / 1e12 if avg_scan_s > 0 else 0.0
 
+    # the reference's call pattern hands host buffers over: same search with numpy queries in
+    # and numpy results out (PCIe both ways + the final sync), reported beside value, never as it
+    host_path = None
+    if world == 1:
+        qh = q.cpu().numpy()
+        index.search(qh, TOPK)
+        t0 = time.perf_counter()
+        n_host = max(3, args.steps // 2)
+        for _ in range(n_host):
+            index.search(qh, TOPK)
+        dt_host = time.perf_counter() - t0
+        host_path = {"queries_per_s": round(NQ * n_host / dt_host, 1), "ms_per_search": round(dt_host / n_host * 1e3, 4),
+                     "note": "numpy queries in / numpy results out (PCIe-inclusive, host buffers); not `value`"}
+
     fusion = None
     if not args.no_fusion:  # config 5 (all ranks take part: sharded corpora + all-gathers)
         del sharded
@@ -376,6 +390,8 @@ def main():
                 if not args.no_cpu_baseline:
                     clip["cpu_baseline"] = clip_cpu_baseline()
                 out["clip"] = clip
+        if host_path is not None:
+            out["host_buffer_path"] = host_path
         if fusion is not None:
             out["fusion"] = fusion
         if not args.no_cpu_baseline and world == 1:
