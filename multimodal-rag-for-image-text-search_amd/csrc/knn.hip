@@ -745,7 +745,10 @@ __device__ __forceinline__ void mfma16_guard(f32x4 (&acc)[4][4]) {
 }
 
 // ABL (timing only, env MRAG_SCAN_ABLATE=20+ABL): 1 = no epilogue, 4 = no epilogue, no LDS-DMA.
-template <int DP, int ABL = 0, int MODE = 0>
+// FRONT = LDS-DMA pieces of the next tile issued per k-step (1, 2 or 4): with FRONT > 1 all of
+// them go out in the first 1/FRONT of the tile, so the last piece has the rest of the tile to
+// land before the end-of-tile vmcnt(0) + barrier (FRONT 1: the last one right before that wait)
+template <int DP, int ABL = 0, int MODE = 0, int FRONT = 4>
 __global__ __launch_bounds__(SCAN2_THREADS) void knn_scan3_kernel(ScanParams p) {
   constexpr int KSTEPS = DP / 32;
   constexpr int ROW_BYTES = DP * 2;
@@ -919,17 +922,19 @@ __global__ __launch_bounds__(SCAN2_THREADS) void knn_scan3_kernel(ScanParams p) 
         // one job per MFMA gap
         if constexpr ((j & 3) == 3) {  // after the last MFMA of block rb: its next fragment
           if constexpr (kk + 1 < KSTEPS) read_a(kk + 1, rb);
-        } else if constexpr (j == 1) {
-          if constexpr (CPR == 64 && !NO_GLDS) {
-            voff = (lane16 ^ (uint32_t)(kk << 4)) + (uint32_t)(kk * 1024);
-            asm volatile("s_mov_b32 m0, %1" : "+v"(voff) : "s"(ldsw + kk * 1024));
+        } else if constexpr ((j & 3) == 1) {  // piece FRONT kk + (j >> 2): m0 + source offset
+          constexpr int pc = FRONT * kk + (j >> 2);
+          if constexpr (CPR == 64 && !NO_GLDS && (j >> 2) < FRONT && pc < GLDS_PER_WAVE) {
+            voff = (lane16 ^ (uint32_t)(pc << 4)) + (uint32_t)(pc * 1024);
+            asm volatile("s_mov_b32 m0, %1" : "+v"(voff) : "s"(ldsw + pc * 1024));
           }
-        } else if constexpr (j == 2) {
-          if constexpr (!NO_GLDS) {
+        } else if constexpr ((j & 3) == 2) {  // ... and its DMA
+          constexpr int pc = FRONT * kk + (j >> 2);
+          if constexpr (!NO_GLDS && (j >> 2) < FRONT && pc < GLDS_PER_WAVE) {
             if constexpr (CPR == 64)
               asm volatile("global_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(gw) : "memory");
             else
-              stage_piece(Y, ntile, kk, lane_t);
+              stage_piece(Y, ntile, pc, lane_t);
           }
         } else if constexpr ((j & 3) == 0) {
           if constexpr (g0 + (j >> 2) < g1)
@@ -1528,7 +1533,15 @@ scan_fn get_scan3(int DP, bool sample = false) {
     case 128: return sample ? knn_scan3_kernel<128, 0, 1> : knn_scan3_kernel<128>;
     case 256: return sample ? knn_scan3_kernel<256, 0, 1> : knn_scan3_kernel<256>;
     case 384: return sample ? knn_scan3_kernel<384, 0, 1> : knn_scan3_kernel<384>;
-    case 512: return sample ? knn_scan3_kernel<512, 0, 1> : knn_scan3_kernel<512>;
+    case 512: {
+      static const int front = [] {  // env MRAG_SCAN_FRONT=1/2: DMA pieces per k-step (A/B timing)
+        const char* e = getenv("MRAG_SCAN_FRONT");
+        return e ? atoi(e) : 4;
+      }();
+      if (front == 1) return sample ? knn_scan3_kernel<512, 0, 1, 1> : knn_scan3_kernel<512, 0, 0, 1>;
+      if (front == 2) return sample ? knn_scan3_kernel<512, 0, 1, 2> : knn_scan3_kernel<512, 0, 0, 2>;
+      return sample ? knn_scan3_kernel<512, 0, 1> : knn_scan3_kernel<512>;
+    }
     default: return nullptr;
   }
 }
