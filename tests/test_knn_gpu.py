@@ -268,3 +268,25 @@ print("ok")
                           root, os.path.join(root, "tests")], env=dict(os.environ, **env), capture_output=True,
                          text=True, timeout=280)
     assert res.returncode == 0 and "ok" in res.stdout, res.stderr[-2000:]
+
+
+def test_lane_list_overflow_bound(cuda):
+    """Adversarial layout for K7 v3's per-lane lists: 45 near-duplicates of query 0 planted on
+    the rows one lane group of one split sees (tiles 0, 256, 512 of a 256-split scan, rows
+    16 rb + r with r < 4), so that lane's list of 6 overflows and most true neighbours are
+    dropped before the fold; part_tau must keep K8's certificate honest (the collect pass then
+    finds them). Results must equal the oracle."""
+    from app.vector_store import FlatIndex
+
+    rng = np.random.default_rng(31)
+    n, d = 40_000, 512
+    x = rng.standard_normal((n, d)).astype(np.float32)
+    q = rng.standard_normal((1, d)).astype(np.float32)
+    rows = [t * 64 + 16 * rb + r for t in (0, 256, 512) for rb in range(4) for r in range(4)][:45]
+    x[rows] = q + 0.02 * rng.standard_normal((len(rows), d)).astype(np.float32)
+    ix = FlatIndex(d)
+    ix.add(x)
+    for k in (1, 5, 10, 40, 50):
+        s, r = ix.search(q, k)
+        os_, or_ = flat_cosine_topk(x, np.zeros(n), q, k)
+        _check(s, r, os_, or_)
