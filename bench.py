@@ -33,6 +33,9 @@ for p in (PKG, ROOT):
     if p not in sys.path:
         sys.path.insert(0, p)
 
+# synthetic encoder weights (random-init architecture; no hub checkpoints offline)
+os.environ.setdefault("MRAG_SYNTHETIC_WEIGHTS", "1")
+
 ROWS_PER_GPU = 1 << 20
 DIM = 512
 NQ = 1000

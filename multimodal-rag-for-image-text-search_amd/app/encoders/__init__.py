@@ -23,7 +23,7 @@ from app.encoders.weights import (
     MINILM_L6,
     MSMARCO_MINILM_L6_CE,
     EncoderConfig,
-    checkpoint_state_dict,
+    encoder_weights,
     param_specs,
     synth_state_dict,
 )
@@ -184,9 +184,12 @@ def gemm_nt(A, W, bias, C, epilogue: int):
     return C
 
 
-def load_encoder(cfg: EncoderConfig, model_path: Optional[str] = None, device: int = 0, seed: int = 0) -> GpuEncoder:
-    """Encoder from a local checkpoint directory when given, else synthetic weights."""
-    sd = checkpoint_state_dict(model_path, cfg) if model_path else None
+def load_encoder(cfg: EncoderConfig, model_name: Optional[str] = None, device: int = 0, seed: int = 0,
+                 synthetic: Optional[bool] = None) -> GpuEncoder:
+    """Encoder for a model name (local directory or cached hub snapshot). Synthetic weights
+    only when ``MRAG_SYNTHETIC_WEIGHTS=1``; otherwise an unresolvable name raises before
+    the GPU is touched (weights.encoder_weights)."""
+    sd, _ = encoder_weights(cfg, model_name, synthetic)
     return GpuEncoder(cfg, device=device, state_dict=sd, seed=seed)
 
 

@@ -21,14 +21,31 @@ import numpy as np
 from app.encoders import CLIP_TEXT_B32, CLIP_VISION_B32, MINILM_L6, load_encoder
 from app.encoders.preprocess import load_batch, load_batch_device
 from app.encoders.tokenize import ClipTokenizer, WordPieceTokenizer
+from app.encoders.weights import resolve_model_dir, synthetic_allowed, SYNTHETIC_ENV
 
 
 def _device_index() -> int:
     return int(os.environ.get("MRAG_DEVICE", "0"))
 
 
-def _local_dir(name: Optional[str]) -> Optional[str]:
-    return name if name and os.path.isdir(name) else None
+def _model_dir(name: Optional[str], need: Sequence[Sequence[str]] = (), synthetic: Optional[bool] = None) -> Optional[str]:
+    """Local directory of a model name (directory or cached hub snapshot), checked for the
+    tokenizer files in ``need`` (any one group complete). None only when synthetic
+    weights are explicitly requested; otherwise an unresolvable name raises like the
+    reference's hub loaders (app/ml/embeddings.py:23-43)."""
+    d = resolve_model_dir(name)
+    if d is None:
+        if synthetic_allowed() if synthetic is None else synthetic:
+            return None
+        raise OSError(f"model {name!r} is neither a local checkpoint directory nor in the local Hugging Face "
+                      f"cache (no network here); set {SYNTHETIC_ENV}=1 for synthetic weights")
+    if need and not any(all(os.path.exists(os.path.join(d, f)) for f in grp) for grp in need):
+        raise FileNotFoundError(f"{d} has no tokenizer files (one of {[list(g) for g in need]})")
+    return d
+
+
+_WORDPIECE_FILES = (("vocab.txt",),)
+_CLIP_BPE_FILES = (("vocab.json", "merges.txt"),)
 
 
 class BatchInputs(dict):
@@ -46,7 +63,7 @@ class BatchInputs(dict):
 
 class MiniLMSentenceModel:
     def __init__(self, name: Optional[str] = None, device: Optional[int] = None):
-        d = _local_dir(name)
+        d = _model_dir(name, _WORDPIECE_FILES)
         self.device = _device_index() if device is None else device
         self.enc = load_encoder(MINILM_L6, d, device=self.device)
         self.tokenizer = WordPieceTokenizer(d, max_len=256)
@@ -77,7 +94,7 @@ class MiniLMSentenceModel:
 
 class ClipModel:
     def __init__(self, name: Optional[str] = None, device: Optional[int] = None):
-        self.dir = _local_dir(name)
+        self.dir = _model_dir(name)  # raises here, as CLIPModel.from_pretrained would
         self.device = _device_index() if device is None else device
         self._vision = None
         self._text = None
@@ -129,7 +146,7 @@ class ClipModel:
 
 class ClipProcessor:
     def __init__(self, name: Optional[str] = None):
-        self.tokenizer = ClipTokenizer(_local_dir(name))
+        self.tokenizer = ClipTokenizer(_model_dir(name, _CLIP_BPE_FILES))
 
     def to(self, device):
         return self
@@ -160,13 +177,13 @@ class CrossEncoderModel:
     label / Identity for several — sentence-transformers' rule."""
 
     def __init__(self, model_name_or_path: Optional[str] = None, max_length: Optional[int] = None,
-                 device: Optional[int] = None, seed: int = 0):
+                 device: Optional[int] = None, seed: int = 0, synthetic: Optional[bool] = None):
         from app.encoders.weights import MSMARCO_MINILM_L6_CE
 
-        d = _local_dir(model_name_or_path)
+        d = _model_dir(model_name_or_path, _WORDPIECE_FILES, synthetic)
         self.device = _device_index() if device is None else device
         self.cfg = MSMARCO_MINILM_L6_CE
-        self.enc = load_encoder(self.cfg, d, device=self.device, seed=seed)
+        self.enc = load_encoder(self.cfg, d, device=self.device, seed=seed, synthetic=d is None)
         self.tokenizer = WordPieceTokenizer(d, max_len=max_length or self.cfg.max_positions)
         self.num_labels = self.cfg.proj_dim
         act = None

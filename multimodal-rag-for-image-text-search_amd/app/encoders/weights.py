@@ -5,12 +5,16 @@ The reference loads pretrained weights by hub name (``config.py:10-12``:
 reachable offline. Parameters therefore come from one of two sources, both keyed by
 the Hugging Face state-dict names the C ABI expects:
 
-* a local checkpoint directory (``model.safetensors``) when ``MODEL_CLIP`` /
-  ``MODEL_TEXT`` points at one (drop-in for real deployments);
-* otherwise a deterministic synthetic generator: a counter-based splitmix64 stream
-  per parameter name, so the GPU box, the oracle and the golden fixtures all see
-  bit-identical weights without shipping 600 MB. Throughput does not depend on the
-  weight values; parity is defined on identical weights (SURVEY.md §7 hard part 2).
+* a local checkpoint (``model.safetensors`` or ``pytorch_model.bin``) when ``MODEL_CLIP``
+  / ``MODEL_TEXT`` names a directory or a hub id cached locally (drop-in for real
+  deployments);
+* only on explicit request (``MRAG_SYNTHETIC_WEIGHTS=1``) a deterministic synthetic
+  generator: a counter-based splitmix64 stream per parameter name, so the GPU box, the
+  oracle and the golden fixtures all see bit-identical weights without shipping 600 MB.
+  Throughput does not depend on the weight values; parity is defined on identical
+  weights (SURVEY.md §7 hard part 2).
+
+Anything else raises, as the reference's loaders do.
 """
 from __future__ import annotations
 
@@ -168,24 +172,98 @@ def synth_state_dict(cfg: EncoderConfig, seed: int = 0) -> Iterator[Tuple[str, n
         yield name, synth_param(name, shape, kind, seed)
 
 
-def checkpoint_state_dict(path: str, cfg: EncoderConfig) -> Optional[Dict[str, np.ndarray]]:
-    """Read a local Hugging Face checkpoint (safetensors) if `path` is a directory
-    holding one; None otherwise. Only the names param_specs() lists are returned."""
-    if not path or not os.path.isdir(path):
-        return None
-    files = [f for f in os.listdir(path) if f.endswith(".safetensors")]
-    if not files:
-        return None
-    from safetensors.numpy import load_file
+SYNTHETIC_ENV = "MRAG_SYNTHETIC_WEIGHTS"
 
+
+def synthetic_allowed() -> bool:
+    """Synthetic weights are an explicit opt-in (benchmarks, tests): ``MRAG_SYNTHETIC_WEIGHTS=1``."""
+    return os.environ.get(SYNTHETIC_ENV) == "1"
+
+
+def _hub_caches() -> List[str]:
+    env = os.environ
+    out = [env.get("HF_HUB_CACHE"), env.get("HUGGINGFACE_HUB_CACHE"), env.get("SENTENCE_TRANSFORMERS_HOME")]
+    if env.get("HF_HOME"):
+        out.append(os.path.join(env["HF_HOME"], "hub"))
+    out.append(os.path.join(os.path.expanduser("~"), ".cache", "huggingface", "hub"))
+    return [c for c in out if c]
+
+
+def resolve_model_dir(name: Optional[str]) -> Optional[str]:
+    """A local directory for a model name: the name itself when it is a directory, else the
+    snapshot of that hub id in the local Hugging Face cache (``models--org--name/snapshots``,
+    the revision ``refs/main`` names first). None when neither exists — there is no network."""
+    if not name:
+        return None
+    if os.path.isdir(name):
+        return name
+    for cache in _hub_caches():
+        repo = os.path.join(cache, "models--" + name.replace("/", "--"))
+        snaps = os.path.join(repo, "snapshots")
+        if not os.path.isdir(snaps):
+            continue
+        ref = os.path.join(repo, "refs", "main")
+        if os.path.isfile(ref):
+            with open(ref) as f:
+                d = os.path.join(snaps, f.read().strip())
+            if os.path.isdir(d):
+                return d
+        revs = sorted((os.path.join(snaps, r) for r in os.listdir(snaps)), key=os.path.getmtime, reverse=True)
+        if revs:
+            return revs[0]
+    return None
+
+
+def _checkpoint_tensors(path: str) -> Iterator[Tuple[str, np.ndarray]]:
+    """(name, array) of every tensor in a checkpoint directory: ``*.safetensors``, else
+    ``pytorch_model*.bin`` through ``torch.load(weights_only=True)`` (never unpickles code)."""
+    st = sorted(f for f in os.listdir(path) if f.endswith(".safetensors"))
+    if st:
+        from safetensors.numpy import load_file
+
+        for f in st:
+            yield from load_file(os.path.join(path, f)).items()
+        return
+    bins = sorted(f for f in os.listdir(path) if f.startswith("pytorch_model") and f.endswith(".bin"))
+    if not bins:
+        raise FileNotFoundError(f"{path} holds no model.safetensors or pytorch_model.bin")
+    import torch
+
+    for f in bins:
+        sd = torch.load(os.path.join(path, f), map_location="cpu", weights_only=True)
+        for k, v in sd.items():
+            yield k, v.detach().to(torch.float32).numpy()
+
+
+def checkpoint_state_dict(path: str, cfg: EncoderConfig) -> Dict[str, np.ndarray]:
+    """Read a local Hugging Face checkpoint directory (safetensors or pytorch_model.bin).
+    Only the names param_specs() lists are returned; a missing file or parameter raises."""
+    if not path or not os.path.isdir(path):
+        raise FileNotFoundError(f"checkpoint directory {path!r} does not exist")
     want = {n for n, _, _ in param_specs(cfg)}
     out: Dict[str, np.ndarray] = {}
-    for f in sorted(files):
-        for k, v in load_file(os.path.join(path, f)).items():
-            for cand in (k, k.replace("0.auto_model.", ""), k.replace("bert.", ""), "bert." + k):
-                if cand in want:
-                    out[cand] = np.asarray(v, dtype=np.float32)
+    for k, v in _checkpoint_tensors(path):
+        for cand in (k, k.replace("0.auto_model.", ""), k.replace("bert.", ""), "bert." + k):
+            if cand in want:
+                out[cand] = np.asarray(v, dtype=np.float32)
     missing = want - set(out)
     if missing:
         raise ValueError(f"checkpoint {path} lacks {len(missing)} parameters, e.g. {sorted(missing)[:3]}")
     return out
+
+
+def encoder_weights(cfg: EncoderConfig, name: Optional[str],
+                    synthetic: Optional[bool] = None) -> Tuple[Optional[Dict[str, np.ndarray]], Optional[str]]:
+    """(state dict, model directory) for a model name, as the reference's ``from_pretrained``
+    / ``SentenceTransformer(name)`` would load it (app/ml/embeddings.py:23-43): a local
+    directory or a cached hub snapshot. Where the reference would fail to load — an
+    unresolvable name offline — this raises too, unless synthetic weights are requested
+    explicitly (``MRAG_SYNTHETIC_WEIGHTS=1``, or ``synthetic=True``: returns ``(None, None)``)."""
+    d = resolve_model_dir(name)
+    if d is not None:
+        return checkpoint_state_dict(d, cfg), d
+    if synthetic_allowed() if synthetic is None else synthetic:
+        return None, None
+    raise OSError(f"model {name!r} is neither a local checkpoint directory nor in the local Hugging Face cache "
+                  f"(no network here); point MODEL_TEXT / MODEL_CLIP / RERANKER_MODEL at a checkpoint directory, "
+                  f"or set {SYNTHETIC_ENV}=1 for deterministic synthetic weights (benchmarks, tests)")

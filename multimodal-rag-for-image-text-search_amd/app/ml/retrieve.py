@@ -8,9 +8,10 @@ order. ``retrieve`` (:103-117): optional cross-encoder rerank + z-score fusion
 ``get_index_version`` are looked up at call time (test seams, tests/test_retrieve.py).
 
 The cross-encoder (ms-marco-MiniLM-L-6) runs on the GPU (``CrossEncoderModel``,
-MRAG_ENC_BERT_PAIR) when RERANKER_MODEL is a local checkpoint directory (or
-MRAG_SYNTHETIC_RERANKER=1); a hub name offline returns False exactly as the reference
-does when the load fails (:29-38), and rerank is skipped. For many queries at once use
+MRAG_ENC_BERT_PAIR) when RERANKER_MODEL is a local checkpoint directory or cached hub
+snapshot (or MRAG_SYNTHETIC_RERANKER=1: synthetic weights, benchmarks / tests); an
+unresolvable name offline returns False exactly as the reference does when the load
+fails (:29-38), and rerank is skipped. For many queries at once use
 ``app.retrieval`` (batched GPU search).
 """
 from __future__ import annotations
@@ -50,15 +51,20 @@ def _get_cross_encoder():
 
 def _gpu_cross_encoder():
     """The GPU cross-encoder when its weights exist locally (RERANKER_MODEL = a checkpoint
-    directory) or synthetic weights are requested (MRAG_SYNTHETIC_RERANKER=1, benchmarks /
-    tests); otherwise False — the reference's outcome when the hub model cannot load."""
+    directory or cached hub snapshot) or synthetic reranker weights are requested
+    (MRAG_SYNTHETIC_RERANKER=1, benchmarks / tests); otherwise False — the reference's
+    outcome when the hub model cannot load. The reranker has its own opt-in because the
+    reference's offline behaviour here is "no rerank", not an error."""
+    from app.encoders.weights import resolve_model_dir
+
     name = settings.models.reranker
-    if not (os.path.isdir(name) or os.environ.get("MRAG_SYNTHETIC_RERANKER") == "1"):
+    synthetic = os.environ.get("MRAG_SYNTHETIC_RERANKER") == "1"
+    if resolve_model_dir(name) is None and not synthetic:
         return False
     try:
         from app.encoders.models import CrossEncoderModel
 
-        return CrossEncoderModel(name)
+        return CrossEncoderModel(name, synthetic=synthetic)
     except Exception:
         return False
 

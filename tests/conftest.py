@@ -14,6 +14,9 @@ import pytest
 
 # the compat layer reads LANCEDB_DIR at import time (as the reference's settings do)
 os.environ.setdefault("LANCEDB_DIR", tempfile.mkdtemp(prefix="mrag_lancedb_"))
+# no hub weights offline: the drop-in encoders raise on an unresolvable model name unless
+# synthetic weights are requested explicitly (tests that check the raise unset this)
+os.environ.setdefault("MRAG_SYNTHETIC_WEIGHTS", "1")
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "multimodal-rag-for-image-text-search_amd")
