@@ -15,7 +15,7 @@ import numpy as np
 import pytest
 from PIL import Image
 
-from conftest import GOLDEN
+from conftest import GOLDEN, record_numerics
 from _data import unit_rows
 from oracle.knn import flat_cosine_topk
 from oracle.normalize import store_normalize
@@ -74,8 +74,10 @@ def test_embed_images_batch_matches_reference_output(cuda, tmp_path):
         paths.append(p)
     got = embeddings.embed_images_batch(paths)
     exp = g["expected"]
-    cos = np.sum(got * exp, 1) / (np.linalg.norm(got, axis=1) * np.linalg.norm(exp, axis=1))
-    assert got.shape == (3, 512) and cos.min() >= 0.9995 and np.abs(got - exp).max() <= 1.5e-2
+    from test_encoders_gpu import ABS_MAX, COS_ERR_MAX
+
+    row = record_numerics("embed_images_batch_vs_reference", got, exp)
+    assert got.shape == (3, 512) and row["max_1_minus_cos"] <= COS_ERR_MAX and row["max_abs_diff"] <= ABS_MAX, row
     assert np.allclose(np.linalg.norm(got, axis=1), 1.0, atol=1e-6)
 
 

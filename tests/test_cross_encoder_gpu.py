@@ -13,7 +13,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import GOLDEN
+from conftest import GOLDEN, record_numerics
 
 pytestmark = pytest.mark.gpu
 
@@ -30,6 +30,8 @@ def ce(cuda):
 def test_logits_golden(ce):
     g = np.load(os.path.join(GOLDEN, "golden_cross_encoder.npz"))
     got = ce.enc.score_pairs(g["ids"], g["types"], g["mask"])
+    record_numerics("cross_encoder_logits", got, g["logits"], unit=False,
+                    logit_spread=float(np.ptp(g["logits"])))
     np.testing.assert_allclose(got, g["logits"], rtol=0, atol=ATOL)
     # a padded row scores like the same row alone (mask + [CLS] pooling)
     one = ce.enc.score_pairs(g["ids"][2:3, :12], g["types"][2:3, :12], g["mask"][2:3, :12])

@@ -1,11 +1,12 @@
 """Parity of the HIP encoders (libmrag.so via the C ABI) with the golden fixtures
 produced by the reference's own code (oracle/gen_golden.py).
 
-Tolerance: the GPU path computes in fp16 MFMA with f32 accumulation and an f32
-residual stream; the reference runs fp32. Unit-norm outputs are required to agree to
-cosine >= 0.9995 and max |diff| <= 1.5e-2 per component; the unnormalised features to
-2% relative L2 error. The K3 GEMM is checked against a torch fp32 product of the same
-fp16 inputs to 1e-2 relative.
+Tolerance (north_star: "cosine scores within 1e-4 fp32"): the GPU path computes in fp16
+MFMA with f32 accumulation and an f32 residual stream; the reference runs fp32. Unit-norm
+outputs must agree row by row to 1 - cos <= 1e-4 and max |diff| <= ABS_MAX per component;
+the unnormalised features to REL_L2 relative L2 error. Every comparison's observed
+errors are recorded (conftest.record_numerics) and printed at the end of the run. The K3
+GEMM is checked against a torch fp32 product of the same fp16 inputs to 1e-2 relative.
 """
 from __future__ import annotations
 
@@ -14,25 +15,22 @@ import os
 import numpy as np
 import pytest
 
-from conftest import GOLDEN
+from conftest import GOLDEN, record_numerics
 
 pytestmark = pytest.mark.gpu
 
-COS_MIN = 0.9995
-ABS_MAX = 1.5e-2
-REL_L2 = 2e-2
+COS_ERR_MAX = 1e-4   # 1 - cos(gpu row, oracle row), north_star
+ABS_MAX = 3e-3       # per component of a unit row (typical component ~0.044 at 512-d)
+REL_L2 = 1.5e-2      # unnormalised features
 
 
-def _cmp(got, exp, unit=True):
-    got = np.asarray(got, np.float64)
-    exp = np.asarray(exp, np.float64)
+def _cmp(got, exp, unit=True, name="encoder"):
+    row = record_numerics(name, got, exp, unit=unit)
     if unit:
-        cos = np.sum(got * exp, 1) / (np.linalg.norm(got, axis=1) * np.linalg.norm(exp, axis=1))
-        assert cos.min() >= COS_MIN, cos
-        assert np.abs(got - exp).max() <= ABS_MAX
+        assert row["max_1_minus_cos"] <= COS_ERR_MAX, row
+        assert row["max_abs_diff"] <= ABS_MAX, row
     else:
-        rel = np.linalg.norm(got - exp, axis=1) / np.linalg.norm(exp, axis=1)
-        assert rel.max() <= REL_L2, rel
+        assert row["max_rel_l2"] <= REL_L2, row
 
 
 @pytest.mark.parametrize("epi", [0, 1, 2, 3, 4])
@@ -110,8 +108,9 @@ def vision(cuda):
 
 def test_clip_image_golden(vision):
     g = np.load(os.path.join(GOLDEN, "golden_clip_image.npz"))
-    _cmp(vision.embed_images(g["images_u8"]), g["expected"])
-    _cmp(vision.embed_images(g["images_u8"], normalize=False), g["expected_unnormalized"], unit=False)
+    _cmp(vision.embed_images(g["images_u8"]), g["expected"], name="clip_image_golden")
+    _cmp(vision.embed_images(g["images_u8"], normalize=False), g["expected_unnormalized"], unit=False,
+         name="clip_image_golden_unnormalized")
 
 
 def test_clip_image_device_batch_consistency(vision, cuda):
@@ -131,8 +130,9 @@ def test_clip_text_golden(cuda):
 
     g = np.load(os.path.join(GOLDEN, "golden_clip_text.npz"))
     enc = GpuEncoder(CLIP_TEXT_B32)
-    _cmp(enc.embed_tokens(g["ids"], g["mask"]), g["expected"])
-    _cmp(enc.embed_tokens(g["ids"], g["mask"], normalize=False), g["expected_unnormalized"], unit=False)
+    _cmp(enc.embed_tokens(g["ids"], g["mask"]), g["expected"], name="clip_text_golden")
+    _cmp(enc.embed_tokens(g["ids"], g["mask"], normalize=False), g["expected_unnormalized"], unit=False,
+         name="clip_text_golden_unnormalized")
 
 
 def test_minilm_golden(cuda):
@@ -140,8 +140,9 @@ def test_minilm_golden(cuda):
 
     g = np.load(os.path.join(GOLDEN, "golden_minilm.npz"))
     enc = GpuEncoder(MINILM_L6)
-    _cmp(enc.embed_tokens(g["ids"], g["mask"]), g["expected"])
-    _cmp(enc.embed_tokens(g["ids"], g["mask"], normalize=False), g["expected_unnormalized"], unit=False)
+    _cmp(enc.embed_tokens(g["ids"], g["mask"]), g["expected"], name="minilm_golden")
+    _cmp(enc.embed_tokens(g["ids"], g["mask"], normalize=False), g["expected_unnormalized"], unit=False,
+         name="minilm_golden_unnormalized")
 
 
 def test_minilm_max_length_256(cuda):
@@ -155,7 +156,7 @@ def test_minilm_max_length_256(cuda):
     mask = np.ones_like(ids)
     mask[1, 200:] = 0
     enc = GpuEncoder(MINILM_L6)
-    _cmp(enc.embed_tokens(ids, mask), minilm_embeds(bert_model(0), ids, mask))
+    _cmp(enc.embed_tokens(ids, mask), minilm_embeds(bert_model(0), ids, mask), name="minilm_L256")
 
 
 def test_gemm_cfg1_128x384_forced(cuda):

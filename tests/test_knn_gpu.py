@@ -163,9 +163,8 @@ def test_l2norm_bit_exact(cuda):
 
 
 def test_full_size_1m_x_512(cuda):
-    """BASELINE config 3 shape: 1M x 512 corpus, 1000 queries, k=10. Every query is
-    checked for sortedness and self-consistency; 32 sampled queries against the
-    exact oracle."""
+    """BASELINE config 3 shape: 1M x 512 corpus, 1000 queries, k=10: every query against
+    the exact oracle (bit-exact rows, f32 scores), plus sortedness of the f64 scores."""
     import torch
     from app.vector_store import FlatIndex
 
@@ -182,9 +181,8 @@ def test_full_size_1m_x_512(cuda):
     assert np.all(np.diff(s64, axis=1) <= 0)
     xh = x.cpu().numpy()
     qh = q.cpu().numpy()
-    sel = np.arange(0, 1000, 1000 // 32)[:32]
-    os_, or_ = flat_cosine_topk(xh, np.zeros(len(xh)), qh[sel], 10)
-    _check(s.cpu().numpy()[sel], r[sel], os_, or_)
+    os_, or_ = flat_cosine_topk(xh, np.zeros(len(xh)), qh, 10)
+    _check(s.cpu().numpy(), r, os_, or_)
     unc, _ = ix.last_stats()
     assert unc == 0
 
