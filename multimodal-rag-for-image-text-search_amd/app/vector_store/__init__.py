@@ -21,6 +21,8 @@ from app import _native
 
 ArrayLike = Union[np.ndarray, "torch.Tensor"]  # noqa: F821
 
+MAX_DIM = 4096  # K7/K8 fused scan up to 512; K7g (knn_generic.hip) above
+MAX_K = 65536
 LABEL_ANY = _native.MRAG_LABEL_ANY
 LABEL_DELETED = _native.MRAG_LABEL_DELETED
 
@@ -45,8 +47,8 @@ class FlatIndex:
     """
 
     def __init__(self, dim: int, device: int = 0) -> None:
-        if not (1 <= int(dim) <= 512):
-            raise ValueError(f"dim must be in 1..512, got {dim}")
+        if not (1 <= int(dim) <= MAX_DIM):
+            raise ValueError(f"dim must be in 1..{MAX_DIM}, got {dim}")
         self.dim = int(dim)
         self.device = int(device)
         h = ctypes.c_void_p()

@@ -33,6 +33,7 @@
 #include <vector>
 
 #include "common.h"
+#include "knn_generic.h"
 
 #define AS1 __attribute__((address_space(1)))
 #define AS3 __attribute__((address_space(3)))
@@ -1078,29 +1079,8 @@ __global__ __launch_bounds__(64) void theta_init_kernel(const float* __restrict_
 }
 
 // ---------------------------------------------------------------------------
-// Exact rescoring helper: one aligned 16-lane group computes q.x in f64 — lane `sub` of the
-// group accumulates the float4 chunks sub, sub + 16, ... in ascending order, then a fixed
-// 4-step butterfly: deterministic — and returns the cosine on every lane of the group.
-// 16 candidates per 256-thread block are rescored at once, each row read with 16-byte
-// loads (one 2 KiB row = 8 loads per lane at 512-d, all in flight together).
-__device__ __forceinline__ double exact_cosine16(const float* qs, double qn, const float* __restrict__ x32,
-                                                 const double* __restrict__ xn, int row, int D, int DP, int sub) {
-  const f32x4* xr = (const f32x4*)(x32 + (size_t)row * DP);
-  const f32x4* q4 = (const f32x4*)qs;
-  const int nc = (D + 3) >> 2;  // chunks; DP % 4 == 0, so the last chunk stays inside the row
-  double acc = 0.0;
-#pragma unroll 8
-  for (int c = sub; c < nc; c += 16) {
-    const f32x4 xv = xr[c], qv = q4[c];
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-      if (4 * c + t < D) acc = fma((double)qv[t], (double)xv[t], acc);
-  }
-#pragma unroll
-  for (int off = 8; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
-  const double xnr = xn[row];
-  return (qn > 0.0 && xnr > 0.0) ? acc / (qn * xnr) : 0.0;
-}
+// Exact rescoring: mrag_knn::exact_cosine16 (knn_generic.h), shared with K7g.
+using mrag_knn::exact_cosine16;
 
 struct MergeParams {
   const float* part_s;
@@ -1448,6 +1428,44 @@ __global__ __launch_bounds__(256) void prep_rows_kernel(const float* __restrict_
   if (lane == 0) xn[row] = nrm;
 }
 
+// Row preparation for DP > 512 (K7g widths): same outputs, two passes over the input row.
+__global__ __launch_bounds__(256) void prep_rows_wide_kernel(const float* __restrict__ in, int64_t nin, int D, int DP,
+                                                             int64_t nout, float* __restrict__ x32,
+                                                             double* __restrict__ xn, _Float16* __restrict__ x16) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= nout) return;
+  const bool live = row < nin;
+  double ss = 0.0;
+  for (int d = lane; d < D; d += 64) {
+    const float v = live ? in[row * D + d] : 0.0f;
+    ss = fma((double)v, (double)v, ss);
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) ss += __shfl_xor(ss, off);
+  const double nrm = sqrt(ss);
+  const double inv = nrm > 0.0 ? 1.0 / nrm : 0.0;
+  for (int d = lane; d < DP; d += 64) {
+    const float v = (live && d < D) ? in[row * D + d] : 0.0f;
+    x32[row * DP + d] = v;
+    x16[row * DP + d] = (_Float16)(float)((double)v * inv);
+  }
+  if (lane == 0) xn[row] = nrm;
+}
+
+int launch_prep(const float* in, int64_t nin, int D, int DP, int64_t nout, float* x32, double* xn, _Float16* x16,
+                hipStream_t s) {
+  if (nout <= 0) return MRAG_OK;
+  if (DP <= 512)
+    hipLaunchKernelGGL(prep_rows_kernel, dim3((unsigned)((nout + 3) / 4)), dim3(256), 0, s, in, nin, D, DP, nout,
+                       x32, xn, x16);
+  else
+    hipLaunchKernelGGL(prep_rows_wide_kernel, dim3((unsigned)((nout + 3) / 4)), dim3(256), 0, s, in, nin, D, DP,
+                       nout, x32, xn, x16);
+  MRAG_CHECK_LAUNCH();
+  return MRAG_OK;
+}
+
 __global__ void fill_i32_kernel(int32_t* p, int64_t n, int32_t v) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) p[i] = v;
@@ -1579,7 +1597,7 @@ struct mrag_knn_index {
   bool no_sample = false;  // env MRAG_SCAN_NO_SAMPLE=1: skip the threshold pre-pass (A/B timing)
   bool scan_v2 = false;    // env MRAG_SCAN_V2=1: the 32x32x16 v2 scan instead of v3 (A/B timing)
   int32_t* host_counters = nullptr;  // pinned [2]: fail_cnt, overflow
-  int ccap = 4096;
+  mrag_knn::Workspace gws[8];  // K7g buffers
   int64_t last_uncertified = 0, last_retries = 0;
   // optional scan timing (mrag_knn_profile)
   bool profile = false;
@@ -1593,7 +1611,7 @@ namespace {
 int grow(mrag_knn_index* ix, int64_t need) {
   if (need <= ix->cap) return MRAG_OK;
   int64_t ncap = std::max<int64_t>({(int64_t)TILE_ROWS, ix->cap * 2, need});
-  ncap = (ncap + TILE_ROWS - 1) / TILE_ROWS * TILE_ROWS;
+  ncap = (ncap + 255) / 256 * 256;  // a multiple of the 64-row scan tile and of K7g's 128-column GEMM tile
   DevBuf nx16, nx32, nxn, nlab;
   if (int rc = ensure(nx16, (size_t)ncap * ix->DP * 2)) return rc;
   if (int rc = ensure(nx32, (size_t)ncap * ix->DP * 4)) return rc;
@@ -1632,7 +1650,8 @@ extern "C" {
 int mrag_knn_create(int32_t dim, int32_t device, mrag_knn_index** out) {
   MRAG_REQUIRE(out != nullptr, "out is NULL");
   *out = nullptr;
-  MRAG_REQUIRE(dim >= 1 && dim <= 512, "dim %d unsupported (1..512)", dim);
+  MRAG_REQUIRE(dim >= 1 && dim <= mrag_knn::GENERIC_MAX_DIM, "dim %d unsupported (1..%d)", dim,
+               mrag_knn::GENERIC_MAX_DIM);
   int ndev = 0;
   MRAG_HIP(hipGetDeviceCount(&ndev));
   MRAG_REQUIRE(device >= 0 && device < ndev, "device %d out of range (%d devices)", device, ndev);
@@ -1665,6 +1684,7 @@ int mrag_knn_destroy(mrag_knn_index* ix) {
                       &ix->cand_cnt, &ix->cand, &ix->scratch, &ix->out_s, &ix->out_s64, &ix->out_r,
                       &ix->stage_rows, &ix->stage_labels, &ix->rowlist, &ix->theta, &ix->part_tau})
       release(*b);
+    mrag_knn::release(ix->gws);
     if (ix->host_counters) (void)hipHostFree(ix->host_counters);
     if (ix->ev0) (void)hipEventDestroy(ix->ev0);
     if (ix->ev1) (void)hipEventDestroy(ix->ev1);
@@ -1729,10 +1749,9 @@ int mrag_knn_add(mrag_knn_index* ix, const float* rows, const int32_t* labels, i
     lsrc = (const int32_t*)ix->stage_labels.p;
   }
   const int64_t n0 = ix->n;
-  hipLaunchKernelGGL(prep_rows_kernel, dim3((unsigned)((nrows + 3) / 4)), dim3(256), 0, s, src, nrows,
-                     ix->D, ix->DP, nrows, (float*)ix->x32.p + n0 * ix->DP, (double*)ix->xn.p + n0,
-                     (_Float16*)ix->x16.p + n0 * ix->DP);
-  MRAG_CHECK_LAUNCH();
+  if (int rc = launch_prep(src, nrows, ix->D, ix->DP, nrows, (float*)ix->x32.p + n0 * ix->DP, (double*)ix->xn.p + n0,
+                           (_Float16*)ix->x16.p + n0 * ix->DP, s))
+    return rc;
   MRAG_HIP(hipMemcpyAsync((int32_t*)ix->labels.p + n0, lsrc, (size_t)nrows * 4, hipMemcpyDeviceToDevice, s));
   MRAG_HIP(hipStreamSynchronize(s));
   ix->n += nrows;
@@ -1764,7 +1783,7 @@ int mrag_knn_search(mrag_knn_index* ix, const float* queries, int64_t nq, int32_
                     int64_t* out_rows, int32_t ptr_kind, void* stream_arg) {
   MRAG_REQUIRE(ix != nullptr, "NULL index");
   MRAG_REQUIRE(nq >= 0, "negative query count");
-  MRAG_REQUIRE(k >= 1 && k <= MAX_K, "k=%d unsupported (1..%d)", k, MAX_K);
+  MRAG_REQUIRE(k >= 1 && k <= mrag_knn::GENERIC_MAX_K, "k=%d unsupported (1..%d)", k, mrag_knn::GENERIC_MAX_K);
   MRAG_REQUIRE(label_filter >= MRAG_LABEL_ANY, "label filter %d invalid", label_filter);
   MRAG_REQUIRE(ptr_kind == MRAG_PTR_HOST || ptr_kind == MRAG_PTR_DEVICE, "bad ptr_kind %d", ptr_kind);
   MRAG_REQUIRE(nq < (1 << 24), "too many queries in one call");
@@ -1794,10 +1813,46 @@ int mrag_knn_search(mrag_knn_index* ix, const float* queries, int64_t nq, int32_
   ix->last_uncertified = 0;
   ix->last_retries = 0;
 
+  auto generic_args = [&]() {
+    mrag_knn::GenericSearch ga{};
+    ga.x16 = (const _Float16*)ix->x16.p;
+    ga.x32 = (const float*)ix->x32.p;
+    ga.xn = (const double*)ix->xn.p;
+    ga.labels = (const int32_t*)ix->labels.p;
+    ga.n = ix->n;
+    ga.D = D;
+    ga.DP = DP;
+    ga.q16 = (const _Float16*)ix->q16.p;
+    ga.q32 = (const float*)ix->q32.p;
+    ga.qn = (const double*)ix->qn.p;
+    ga.nq = (int)nq;
+    ga.k = k;
+    ga.label_filter = label_filter;
+    ga.row_offset = row_offset;
+    ga.out_s = os;
+    ga.out_s64 = os64;
+    ga.out_r = orr;
+    return ga;
+  };
+
   if (ix->n == 0) {
     hipLaunchKernelGGL(fill_empty_kernel, dim3((unsigned)((nout + 255) / 256)), dim3(256), 0, s, os, os64,
                        orr, nout);
     MRAG_CHECK_LAUNCH();
+  } else if (DP > 512 || k > MAX_K) {
+    // K7g (knn_generic.hip): widths and depths the fused scan does not instantiate
+    const float* qsrc = queries;
+    if (host) {
+      if (int rc = ensure(ix->qin, (size_t)nq * D * 4)) return rc;
+      MRAG_HIP(hipMemcpyAsync(ix->qin.p, queries, (size_t)nq * D * 4, hipMemcpyHostToDevice, s));
+      qsrc = (const float*)ix->qin.p;
+    }
+    if (int rc = ensure(ix->q32, (size_t)nq * DP * 4)) return rc;
+    if (int rc = ensure(ix->qn, (size_t)nq * 8)) return rc;
+    if (int rc = ensure(ix->q16, (size_t)nq * DP * 2)) return rc;
+    if (int rc = launch_prep(qsrc, nq, D, DP, nq, (float*)ix->q32.p, (double*)ix->qn.p, (_Float16*)ix->q16.p, s))
+      return rc;
+    if (int rc = mrag_knn::search_generic(generic_args(), ix->gws, s, nullptr)) return rc;
   } else {
     // v2 (64 queries/wave, KL = 8) unless k is deep enough to want longer per-lane lists
     // (per-lane lists of 8; for 32 < k <= 64 the union of the S split lists still holds
@@ -1840,9 +1895,8 @@ int mrag_knn_search(mrag_knn_index* ix, const float* queries, int64_t nq, int32_
     if (use_v3)
       if (int rc = ensure(ix->part_tau, (size_t)S * Qp * 4)) return rc;
 
-    hipLaunchKernelGGL(prep_rows_kernel, dim3((unsigned)((Qp + 3) / 4)), dim3(256), 0, s, qsrc, nq, D, DP,
-                       Qp, (float*)ix->q32.p, (double*)ix->qn.p, (_Float16*)ix->q16.p);
-    MRAG_CHECK_LAUNCH();
+    if (int rc = launch_prep(qsrc, nq, D, DP, Qp, (float*)ix->q32.p, (double*)ix->qn.p, (_Float16*)ix->q16.p, s))
+      return rc;
     MRAG_HIP(hipMemsetAsync(ix->counters.p, 0, 16, s));
     MRAG_HIP(hipMemsetAsync(ix->cand_cnt.p, 0, (size_t)Qp * 4, s));
     MRAG_HIP(hipMemsetAsync(ix->theta.p, 0, (size_t)Qp * 4, s));
@@ -1939,11 +1993,16 @@ int mrag_knn_search(mrag_knn_index* ix, const float* queries, int64_t nq, int32_
     hipLaunchKernelGGL(knn_merge_kernel, dim3((unsigned)nq), dim3(MERGE_THREADS), msh, s, mp);
     MRAG_CHECK_LAUNCH();
 
-    for (int attempt = 0;; ++attempt) {
-      if (int rc = ensure(ix->cand, (size_t)Qp * ix->ccap * 4)) return rc;
-      if (int rc = ensure(ix->scratch, (size_t)Qp * ix->ccap * 8)) return rc;
+    {
+      // per-slot collect capacity of this search (K7c/K10 for the uncertified queries): at
+      // most 4096 rows and 64M slots in all; a query that collects more (a run of more than
+      // ccap near-duplicates within eps of its k-th score) sends the batch to K7g below,
+      // whose per-query storage is sized from a histogram — nothing grows across searches
+      const int ccap = (int)std::max<int64_t>(256, std::min<int64_t>(4096, ((int64_t)64 << 20) / Qp));
+      if (int rc = ensure(ix->cand, (size_t)Qp * ccap * 4)) return rc;
+      if (int rc = ensure(ix->scratch, (size_t)Qp * ccap * 8)) return rc;
       sp.cand = (int32_t*)ix->cand.p;
-      sp.ccap = ix->ccap;
+      sp.ccap = ccap;
       hipLaunchKernelGGL(collect, sgrid, dim3(SCAN_THREADS), 0, s, sp);
       MRAG_CHECK_LAUNCH();
       FinalParams fp{};
@@ -1951,7 +2010,7 @@ int mrag_knn_search(mrag_knn_index* ix, const float* queries, int64_t nq, int32_
       fp.fail_cnt = sp.fail_cnt;
       fp.cand_cnt = sp.cand_cnt;
       fp.cand = sp.cand;
-      fp.ccap = ix->ccap;
+      fp.ccap = ccap;
       fp.scratch = (double*)ix->scratch.p;
       fp.q32 = mp.q32;
       fp.qn = mp.qn;
@@ -1970,23 +2029,16 @@ int mrag_knn_search(mrag_knn_index* ix, const float* queries, int64_t nq, int32_
       MRAG_HIP(hipMemcpyAsync(ix->host_counters, ix->counters.p, 8, hipMemcpyDeviceToHost, s));
       MRAG_HIP(hipStreamSynchronize(s));
       ix->last_uncertified = ix->host_counters[0];
-      if (ix->profile && attempt == 0) {
+      if (ix->profile) {
         float ms = 0.f;
         MRAG_HIP(hipEventElapsedTime(&ms, ix->ev0, ix->ev1));
         ix->scan_ms += ms;
         ix->scan_launches++;
       }
-      if (ix->host_counters[1] == 0) break;
-      // some uncertified query collected more rows than ccap: size for the worst one and rerun
-      std::vector<int32_t> cnt((size_t)ix->host_counters[0]);
-      MRAG_HIP(hipMemcpy(cnt.data(), ix->cand_cnt.p, cnt.size() * 4, hipMemcpyDeviceToHost));
-      int mx = 0;
-      for (int32_t c : cnt) mx = std::max(mx, c);
-      MRAG_REQUIRE(attempt < 3, "collect pass did not converge");
-      ix->ccap = (mx + 1023) / 1024 * 1024;
-      ix->last_retries++;
-      MRAG_HIP(hipMemsetAsync(ix->cand_cnt.p, 0, (size_t)Qp * 4, s));
-      MRAG_HIP(hipMemsetAsync((int32_t*)ix->counters.p + 1, 0, 4, s));
+      if (ix->host_counters[1] != 0) {
+        ix->last_retries = 1;
+        if (int rc = mrag_knn::search_generic(generic_args(), ix->gws, s, nullptr)) return rc;
+      }
     }
   }
 
@@ -2001,7 +2053,7 @@ int mrag_knn_search(mrag_knn_index* ix, const float* queries, int64_t nq, int32_
 
 int mrag_topk_merge(const double* scores64, const int64_t* rows, int32_t nlists, int64_t nq, int32_t k,
                     float* out_scores, double* out_scores64, int64_t* out_rows, void* stream) {
-  MRAG_REQUIRE(nlists >= 1 && nq >= 0 && k >= 1 && k <= MAX_K, "bad shape nlists=%d nq=%lld k=%d", nlists,
+  MRAG_REQUIRE(nlists >= 1 && nq >= 0 && k >= 1 && k <= mrag_knn::GENERIC_MAX_K, "bad shape nlists=%d nq=%lld k=%d", nlists,
                (long long)nq, k);
   if (nq == 0) return MRAG_OK;
   MRAG_REQUIRE(scores64 && rows && out_scores && out_rows, "NULL pointer");

@@ -5,7 +5,8 @@ predict() conventions, and the reference's _rerank_text (app/ml/retrieve.py:132-
 GPU model vs the same function on the oracle model.
 
 Tolerance: fp16 GEMM inputs with f32 accumulation through 6 post-LN layers; logits are
-checked to |delta| <= 1e-2 (their spread on these pairs is ~0.6)."""
+checked to |delta| <= 3e-3 (observed 6.2e-4, profiles/r2_numerics.json; their spread on these
+pairs is ~0.6)."""
 from __future__ import annotations
 
 import os
@@ -17,7 +18,7 @@ from conftest import GOLDEN, record_numerics
 
 pytestmark = pytest.mark.gpu
 
-ATOL = 1e-2
+ATOL = 3e-3
 
 
 @pytest.fixture(scope="module")

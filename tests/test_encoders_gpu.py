@@ -19,9 +19,11 @@ from conftest import GOLDEN, record_numerics
 
 pytestmark = pytest.mark.gpu
 
+# Observed on MI355X (profiles/r2_numerics.json): 1 - cos <= 6e-7, |diff| <= 2.3e-4 on unit
+# rows, relative L2 <= 1.1e-3 on unnormalised features, over every tower and BASELINE config.
 COS_ERR_MAX = 1e-4   # 1 - cos(gpu row, oracle row), north_star
-ABS_MAX = 3e-3       # per component of a unit row (typical component ~0.044 at 512-d)
-REL_L2 = 1.5e-2      # unnormalised features
+ABS_MAX = 1e-3       # per component of a unit row (typical component ~0.044 at 512-d)
+REL_L2 = 5e-3        # unnormalised features
 
 
 def _cmp(got, exp, unit=True, name="encoder"):
