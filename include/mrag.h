@@ -70,7 +70,12 @@ int mrag_l2norm_rows(const float* x, float* y, int64_t rows, int32_t dim, void* 
  * (text_collection or image_collection, lancedb_store.py:30-31) or one shard
  * of it. Exact semantics: score = cos(q, x) = q.x / (|q| |x|) evaluated in
  * f64 on the f32 vectors as given (0 if either norm is 0), results ordered by
- * (score desc, row asc), label prefilter, at most k rows. */
+ * (score desc, row asc), label prefilter, at most k rows.
+ * Limits: 1 <= dim <= 4096, 1 <= k <= 65536 (the reference has none: Lance stores
+ * list<float32> of any length, :33-44, and passes limit(max(k,1)) through, :110,121).
+ * dim <= 512 with k <= 256 runs the fused fp16 scan (K7/K8, knn.hip); wider rows and deeper
+ * k run K7g (knn_generic.hip: MFMA score GEMM + histogram threshold + exact selection).
+ * Both are exact. */
 typedef struct mrag_knn_index mrag_knn_index;
 
 int mrag_knn_create(int32_t dim, int32_t device, mrag_knn_index** out);

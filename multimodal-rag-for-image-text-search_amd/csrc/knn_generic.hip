@@ -14,7 +14,7 @@
 //          the same GEMM -> collect every admitted row with approx >= thr;
 //   K7g-f: exact f64 rescoring of the candidates (mrag_knn::exact_cosine16, the same
 //          arithmetic as K8/K10) and ordered selection (score desc, row asc): bitonic sort in
-//          LDS up to 4096 candidates, k rounds of block arg-max beyond.
+//          LDS up to 2048 candidates, k rounds of block arg-max beyond.
 // Exact by construction for every input (duplicates and ties included): the candidate set
 // is a superset of the exact top-k.
 #include <algorithm>
@@ -31,7 +31,7 @@ constexpr int HIST_BINS = 2048;
 constexpr float HIST_LO = -1.0625f;  // scores of unit vectors (plus eps) lie in [-1.0625, 1.0625)
 constexpr float HIST_SPAN = 2.125f;
 constexpr int GF_THREADS = 256;
-constexpr int GF_SORT_MAX = 4096;
+constexpr int GF_SORT_MAX = 2048;  // LDS sort capacity (12 B each; + the query row, <= 40 KiB)
 constexpr size_t SCORE_BUDGET = (size_t)512 << 20;  // bytes of S per chunk
 constexpr int64_t CAND_BUDGET = (int64_t)96 << 20;   // candidates per collect sub-range (12 B each)
 constexpr int QBLOCK = 8192;                          // queries per histogram block
