@@ -32,7 +32,7 @@ def search_batch(modality: str, user_id: str, query_vecs: np.ndarray, top_k: int
     norms = np.linalg.norm(q, axis=1, keepdims=True)
     q = np.where(norms > 0, q / np.where(norms > 0, norms, 1), q).astype(np.float32)
     with table.lock:
-        table._load()  # replay a persisted table on first use in this process
+        table._sync()  # replay what any process committed since the last call
         label = table.labels.get(user_id)
         if table.index is None or label is None:
             return [[] for _ in range(len(q))]

@@ -17,9 +17,18 @@ One directory per table (``<db>/mrag_tables/<table>/``), append-only:
 Global row ids are the concatenation order of the segments, i.e. the GPU index's row ids,
 so a reopened table returns the same rows in the same tie order (score desc, row asc).
 Readers replay only the segments and tombstones the manifest lists.
+
+Several processes share one directory (the reference's Celery worker indexes while the API
+process searches, app/tasks.py:108,165 and api/routes.py:276, both on LANCEDB_DIR): writers
+serialise on an exclusive ``fcntl`` lock of ``<dir>/.lock`` and re-read the manifest under
+it before appending, so segment names and tombstone offsets never collide; readers need no
+lock (the manifest is replaced atomically and lists only durable, immutable bytes) and pick
+up other processes' commits with ``refresh()`` (a stat of the manifest per call).
 """
 from __future__ import annotations
 
+import contextlib
+import fcntl
 import json
 import os
 from dataclasses import dataclass
@@ -52,9 +61,35 @@ class CorpusFiles:
         self.dir = directory
         self.manifest_path = os.path.join(directory, "manifest.json")
         self.manifest: Dict[str, Any] = {"dim": None, "segments": [], "tombstones": 0}
-        if os.path.exists(self.manifest_path):
-            with open(self.manifest_path) as f:
-                self.manifest = json.load(f)
+        self._stamp = None
+        self.refresh()
+
+    def refresh(self) -> bool:
+        """Re-read the manifest if another process committed since the last read (True if so)."""
+        try:
+            st = os.stat(self.manifest_path)
+        except FileNotFoundError:
+            return False
+        stamp = (st.st_ino, st.st_mtime_ns, st.st_size)
+        if stamp == self._stamp:
+            return False
+        with open(self.manifest_path) as f:
+            self.manifest = json.load(f)
+        self._stamp = stamp
+        return True
+
+    @contextlib.contextmanager
+    def write_lock(self):
+        """Exclusive inter-process writer lock; the manifest is fresh inside it."""
+        os.makedirs(self.dir, exist_ok=True)
+        fd = os.open(os.path.join(self.dir, ".lock"), os.O_RDWR | os.O_CREAT, 0o644)
+        try:
+            fcntl.flock(fd, fcntl.LOCK_EX)
+            self.refresh()
+            yield self
+        finally:
+            fcntl.flock(fd, fcntl.LOCK_UN)
+            os.close(fd)
 
     @property
     def dim(self) -> Optional[int]:
@@ -65,7 +100,8 @@ class CorpusFiles:
         return sum(s["rows"] for s in self.manifest["segments"])
 
     def append(self, vectors: np.ndarray, rows: Sequence[Dict[str, Any]], dead: Sequence[int] = ()) -> None:
-        """Durably append one upsert: its tombstones (row ids it replaces) and its rows."""
+        """Durably append one upsert: its tombstones (row ids it replaces) and its rows. Call
+        it inside ``write_lock()`` when other processes may write the same table."""
         import pyarrow as pa
         import pyarrow.parquet as pq
 
@@ -101,22 +137,27 @@ class CorpusFiles:
             m["segments"].append({"name": name, "rows": int(v.shape[0])})
         _fsync_write(self.manifest_path, json.dumps(m).encode())
         self.manifest = m
+        st = os.stat(self.manifest_path)
+        self._stamp = (st.st_ino, st.st_mtime_ns, st.st_size)
 
-    def segments(self) -> Iterator[Segment]:
+    def segments(self, start: int = 0) -> Iterator[Segment]:
+        """The committed segments from index ``start`` on (all by default)."""
         import pyarrow.parquet as pq
 
         dim = self.manifest["dim"]
-        for s in self.manifest["segments"]:
+        for s in self.manifest["segments"][start:]:
             vec = np.memmap(os.path.join(self.dir, s["name"] + ".f32"), dtype="<f4", mode="r",
                             shape=(s["rows"], dim))
             t = pq.read_table(os.path.join(self.dir, s["name"] + ".parquet")).to_pydict()
             yield Segment(vectors=vec, rows=t)
 
-    def tombstones(self) -> np.ndarray:
+    def tombstones(self, start: int = 0) -> np.ndarray:
+        """Committed tombstones from position ``start`` on (all by default)."""
         n = self.manifest["tombstones"]
-        if n == 0:
+        if n <= start:
             return np.empty(0, dtype=np.int64)
-        return np.fromfile(os.path.join(self.dir, "tombstones.i64"), dtype="<i8", count=n).astype(np.int64)
+        return np.fromfile(os.path.join(self.dir, "tombstones.i64"), dtype="<i8", count=n - start,
+                           offset=8 * start).astype(np.int64)
 
 
 __all__ = ["CorpusFiles", "Segment", "COLUMNS"]

@@ -12,13 +12,16 @@ Every ``LanceDBStore`` opened on the same directory shares the same tables (the
 reference's two handles on one directory could miss each other's writes).
 Tables persist under ``<db_path>/mrag_tables/<table>/`` (``app.storage.corpus_files``:
 fp32 row segments + Parquet payloads + tombstones, atomic manifest) and are replayed into
-the GPU index on first use in a new process, with the same row ids.
+the GPU index with the same row ids. Processes sharing the directory (the reference's
+worker indexing while the API searches) see each other's commits: every search and upsert
+first replays what was committed since, and upserts serialise on a file lock.
 Semantics pinned in DESIGN.md §3: exact flat cosine (no IVF_PQ — the reference's
 index build is attempted on an empty table and swallowed, :51-60), prefilter, order
 (score desc, row asc), ``limit(max(top_k, 1))``, ``score = 1 - f32(1 - cos)``.
 """
 from __future__ import annotations
 
+import contextlib
 import json
 import os
 import threading
@@ -41,7 +44,11 @@ class VectorRow:
 
 
 class _Table:
-    """One collection: GPU rows + host-side row payloads (+ their files, if persistent)."""
+    """One collection: GPU rows + host-side row payloads (+ their files, if persistent).
+
+    With files, the in-memory table is a replay of the committed segments and tombstones in
+    manifest order (so row ids agree across processes); ``_sync`` replays what other
+    processes committed since the last call, at the start of every search and upsert."""
 
     def __init__(self, name: str, device: int = 0, directory: Optional[str] = None):
         self.name = name
@@ -51,7 +58,6 @@ class _Table:
             from app.storage.corpus_files import CorpusFiles
 
             self.files = CorpusFiles(directory)
-        self._loaded = self.files is None or self.files.num_rows == 0
         self.index = None  # FlatIndex, created on the first write (dim unknown before)
         self.dim: Optional[int] = None
         self.chunk_ids: List[str] = []
@@ -60,6 +66,8 @@ class _Table:
         self.by_chunk: Dict[str, List[int]] = {}
         self.labels: Dict[str, int] = {}
         self.lock = threading.RLock()
+        self._seen_segments = 0    # committed segments replayed into this process
+        self._seen_tombstones = 0  # committed tombstones applied
 
     def _ensure_index(self, dim: int):
         if self.index is None:
@@ -70,65 +78,70 @@ class _Table:
         elif dim != self.dim:
             raise ValueError(f"{self.name}: embedding dim {dim} != table dim {self.dim}")
 
-    def _load(self) -> None:
-        """Replay the table's segments + tombstones into the GPU index (once per process)."""
-        if self._loaded:
+    def _append_rows(self, vectors: np.ndarray, user_ids, chunk_ids, metas, doc_ids) -> None:
+        labs = np.asarray([self.labels.setdefault(u, len(self.labels)) for u in user_ids], dtype=np.int32)
+        first = self.index.add(np.asarray(vectors), labs)
+        for i, cid in enumerate(chunk_ids):
+            self.chunk_ids.append(cid)
+            self.metas.append(metas[i])
+            self.doc_ids.append(doc_ids[i])
+            self.by_chunk.setdefault(cid, []).append(first + i)
+
+    def _kill_rows(self, dead) -> None:
+        dead = [int(r) for r in dead]
+        if not dead:
             return
-        self._loaded = True
-        self._ensure_index(self.files.dim)
-        for seg in self.files.segments():
-            cols = seg.rows
-            labs = np.asarray([self.labels.setdefault(u, len(self.labels)) for u in cols["user_id"]], dtype=np.int32)
-            first = self.index.add(np.asarray(seg.vectors), labs)
-            for i, cid in enumerate(cols["chunk_id"]):
-                self.chunk_ids.append(cid)
-                self.metas.append(cols["meta"][i])
-                self.doc_ids.append(cols["document_id"][i])
-                self.by_chunk.setdefault(cid, []).append(first + i)
-        dead = self.files.tombstones()
-        if dead.size:
-            self.index.delete(dead)
-            for r in dead.tolist():
-                rows = self.by_chunk.get(self.chunk_ids[r])
-                if rows and r in rows:
-                    rows.remove(r)
-                    if not rows:
-                        del self.by_chunk[self.chunk_ids[r]]
+        self.index.delete(dead)
+        for r in dead:
+            rows = self.by_chunk.get(self.chunk_ids[r])
+            if rows and r in rows:
+                rows.remove(r)
+                if not rows:
+                    del self.by_chunk[self.chunk_ids[r]]
+
+    def _sync(self) -> None:
+        """Replay the segments + tombstones committed (by any process) since the last sync."""
+        if self.files is None:
+            return
+        self.files.refresh()
+        m = self.files.manifest
+        if len(m["segments"]) > self._seen_segments:
+            self._ensure_index(self.files.dim)
+            for seg in self.files.segments(self._seen_segments):
+                c = seg.rows
+                self._append_rows(seg.vectors, c["user_id"], c["chunk_id"], c["meta"], c["document_id"])
+                self._seen_segments += 1
+        if m["tombstones"] > self._seen_tombstones:
+            self._kill_rows(self.files.tombstones(self._seen_tombstones))
+            self._seen_tombstones = m["tombstones"]
+
+    _load = _sync  # name used by app.retrieval
 
     def upsert(self, payloads: List[Dict[str, Any]]) -> None:
         if not payloads:
             return
         with self.lock:
-            self._load()
             emb = np.asarray([p["embedding"] for p in payloads], dtype=np.float32)
             if emb.ndim != 2:
                 raise ValueError("all embeddings in one upsert must have the same length")
-            self._ensure_index(emb.shape[1])
-            # per-row delete of any existing row with the same chunk_id (lancedb_store.py:91-92)
-            dead = []
-            for p in payloads:
-                dead.extend(self.by_chunk.pop(p["chunk_id"], []))
-            if self.files is not None:  # durable first: a failed write leaves the table as it was
-                try:
+            with (self.files.write_lock() if self.files is not None else contextlib.nullcontext()):
+                self._sync()  # under the writer lock: every committed row is visible here
+                self._ensure_index(emb.shape[1])
+                # per-row delete of any existing row with the same chunk_id (lancedb_store.py:91-92)
+                dead = []
+                for p in payloads:
+                    dead.extend(self.by_chunk.get(p["chunk_id"], []))
+                if self.files is not None:  # durable first: a failed write leaves the table as it was
                     self.files.append(emb, payloads, dead)
-                except Exception:
-                    for r in dead:
-                        self.by_chunk.setdefault(self.chunk_ids[r], []).append(r)
-                    raise
-            if dead:
-                self.index.delete(dead)
-            labs = np.asarray([self.labels.setdefault(p["user_id"], len(self.labels)) for p in payloads],
-                              dtype=np.int32)
-            first = self.index.add(emb, labs)
-            for i, p in enumerate(payloads):
-                self.chunk_ids.append(p["chunk_id"])
-                self.metas.append(p["meta"])
-                self.doc_ids.append(p["document_id"])
-                self.by_chunk.setdefault(p["chunk_id"], []).append(first + i)
+                    self._seen_segments += 1
+                    self._seen_tombstones += len(dead)
+                self._kill_rows(dead)
+                self._append_rows(emb, [p["user_id"] for p in payloads], [p["chunk_id"] for p in payloads],
+                                  [p["meta"] for p in payloads], [p["document_id"] for p in payloads])
 
     def search(self, user_id: str, vector: List[float], k: int) -> List[Dict[str, Any]]:
         with self.lock:
-            self._load()
+            self._sync()
             label = self.labels.get(user_id)
             if self.index is None or label is None:
                 return []

@@ -85,7 +85,11 @@ class FlatIndex:
             if labels is None or isinstance(labels, int):
                 lab = torch.full((n,), int(labels or 0), dtype=torch.int32, device=r.device)
             else:
-                lab = labels.to(device=r.device, dtype=torch.int32).contiguous()
+                lab = torch.as_tensor(labels).to(device=r.device, dtype=torch.int32).contiguous()
+                if tuple(lab.shape) != (n,):
+                    raise ValueError(f"labels must be [{n}], got {tuple(lab.shape)}")
+            if n and bool((lab < 0).any()):
+                raise ValueError("labels must be >= 0")
             torch.cuda.current_stream(r.device).synchronize()
             _native.call("mrag_knn_add", self._h, r.data_ptr(), lab.data_ptr(), n,
                          _native.MRAG_PTR_DEVICE, ctypes.byref(first))

@@ -165,3 +165,46 @@ def test_store_persists_across_restart(cuda, tmp_path):
     assert ids[:2] == ["c100", "c5"]  # exact tie: older row first
     assert [h["meta"] for h in hits[:2]] == [{"i": 100}, {"i": "new"}]
     assert again.search_text("u1", vecs[5], 1)[0]["chunk_id"] != "c5"  # the replaced row stays deleted
+
+
+def test_store_sees_other_process(cuda, tmp_path):
+    """a second process (the reference's indexing worker) commits rows to the same
+    LANCEDB_DIR after this process's first search; this process's store must serve them
+    (exact, against the oracle), and its own later upsert must land after them."""
+    import subprocess
+    import sys
+
+    from app.storage import lancedb_store as ls
+
+    db = str(tmp_path / "shared")
+    rng = np.random.default_rng(12)
+    X = rng.standard_normal((400, 128)).astype(np.float32)
+    store = ls.LanceDBStore(db)
+    store.upsert_text_vectors([ls.VectorRow(f"c{i}", "alice", "d", "text", X[i], {"i": i}) for i in range(200)])
+    q = rng.standard_normal(128).astype(np.float32)
+    assert len(store.search_text("alice", q, 300)) == 200
+    code = r'''
+import sys, numpy as np
+sys.path[:0] = [sys.argv[1], sys.argv[2]]
+from app.storage.lancedb_store import LanceDBStore, VectorRow
+X = np.random.default_rng(12).standard_normal((400, 128)).astype(np.float32)
+s = LanceDBStore(sys.argv[3])
+s.upsert_text_vectors([VectorRow(f"c{i}", "alice", "d", "text", X[i], {"i": i}) for i in range(200, 400)])
+s.upsert_text_vectors([VectorRow("c7", "alice", "d", "text", X[399], {"i": "moved"})])
+print("ok")
+'''
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    res = subprocess.run([sys.executable, "-c", code, os.path.join(root, "multimodal-rag-for-image-text-search_amd"),
+                          root, db], capture_output=True, text=True, timeout=240)
+    assert res.returncode == 0 and "ok" in res.stdout, res.stderr[-2000:]
+    stored = np.asarray([store_normalize(x) for x in X], np.float32)
+    stored[7] = store_normalize(X[399])
+    lab = np.zeros(400, np.int64)
+    os_, or_ = flat_cosine_topk(stored, lab, np.asarray([store_normalize(q)], np.float32), 400)
+    got = store.search_text("alice", q, 400)
+    assert [g["chunk_id"] for g in got] == [f"c{r}" for r in or_[0] if r >= 0]
+    assert len(got) == 400 and [g for g in got if g["chunk_id"] == "c7"][0]["meta"] == {"i": "moved"}
+    store.upsert_text_vectors([ls.VectorRow("c8", "alice", "d", "text", X[0], {"i": "mine"})])
+    got = store.search_text("alice", X[0], 2)
+    assert {g["chunk_id"] for g in got} == {"c0", "c8"}
+    ls._REGISTRY.clear()
