@@ -1,10 +1,17 @@
 """Compatibility shim for the reference's dead ``app/embedding/embedder.py`` (:15-68).
 
 Nothing in the reference imports ``Embedder`` except a stale test; it is kept as a thin
-facade over the same GPU encoders so code written against it still runs:
-``embed_text`` -> MiniLM [N,384] (sentence-transformers output, no extra numpy
-normalise), ``embed_text_for_images`` -> CLIP text [N,512], ``embed_images`` -> CLIP
-image [N,512]; empty input -> ``np.empty((0, 0))`` like the reference.
+facade over the same GPU encoders so code written against it still runs. Outputs follow
+what the reference's ``SentenceTransformer(...).encode(convert_to_tensor=True)`` returns
+(sentence-transformers is not installed here, so this is a restatement, parity unpinned):
+
+* ``embed_text`` -> MiniLM [N,384] float32, unit rows (all-MiniLM-L6-v2's pipeline ends in a
+  Normalize module; no extra numpy ``_normalize``);
+* ``embed_text_for_images`` -> CLIP text features [N,512] float32, NOT normalised
+  (sentence-transformers' CLIPModel module returns ``text_embeds`` = the projection);
+* ``embed_images`` -> CLIP image features [N,512] float32, NOT normalised (``image_embeds``);
+* empty input -> ``np.empty((0, 0))`` (float64, as the reference); model-name resolution
+  and errors as ``app.encoders.models`` (an unresolvable name raises).
 """
 from __future__ import annotations
 
@@ -52,12 +59,10 @@ class Embedder:
         if not text_list:
             return np.empty((0, 0))
         inputs = self._proc(text=list(text_list))
-        feats = self._clip.get_text_features(**inputs)
-        return (feats / feats.norm(dim=1, keepdim=True).clamp_min(1e-12)).cpu().numpy()
+        return self._clip.get_text_features(**inputs).cpu().numpy()
 
     def embed_images(self, image_paths: Iterable[str]) -> np.ndarray:
         paths = list(image_paths)
         if not paths:
             return np.empty((0, 0))
-        feats = self._clip.get_image_features(**self._proc(images=paths))
-        return (feats / feats.norm(dim=1, keepdim=True).clamp_min(1e-12)).cpu().numpy()
+        return self._clip.get_image_features(**self._proc(images=paths)).cpu().numpy()

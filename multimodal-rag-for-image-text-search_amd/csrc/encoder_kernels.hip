@@ -50,8 +50,11 @@ __device__ __forceinline__ float gemm_act(float x) {
     // fp16) instead of a full-precision divide
     return x * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.702f * 1.44269504088896341f * x));
   } else if constexpr (EPI == EPI_F16_GELU_ERF) {
-    // erf by Abramowitz & Stegun 7.1.26 (|error| <= 1.5e-7, far below the fp16 rounding of the
-    // result) with hardware rcp / exp2: a fraction of the cost of the libm erff in the epilogue
+    // erf by Abramowitz & Stegun 7.1.26 with hardware rcp / exp2: a fraction of the cost of the
+    // libm erff in the epilogue. The erf error (<= 1.5e-7 absolute) gives a GELU error of at most
+    // 0.5 |x| 1.5e-7 + rcp/exp2 ulps, i.e. an ABSOLUTE bound (~1e-6 at |x| = 8): below the fp16
+    // rounding of outputs of magnitude >~ 2e-3, but several fp16 ulps in the far negative tail
+    // where GELU(x) itself is ~1e-6 (tests/test_encoders_gpu.py::test_gelu_erf_epilogue_sweep)
     const float z = x * 0.70710678118654752f, az = fabsf(z);
     const float t = __builtin_amdgcn_rcpf(1.0f + 0.3275911f * az);
     const float poly =

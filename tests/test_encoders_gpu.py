@@ -197,3 +197,31 @@ print("ok")
                           root], env=env, capture_output=True, text=True, timeout=240)
     assert res.returncode == 0 and "ok" in res.stdout, res.stderr[-2000:]
     assert "K3d cfg 1" in res.stderr
+
+
+def test_gelu_erf_epilogue_sweep(cuda):
+    """the erf-GELU epilogue (A&S 7.1.26 + hardware rcp/exp2) swept over x in
+    [-8, 8) against torch.nn.functional.gelu (exact erf) on the fp16 output, with an absolute
+    bound: fp16 rounding of the result (half an ulp, <= 2^-11 relative) + 2e-6 absolute.
+    x = A[r,0] * W[n,0] + bias[n] = (r/8 - 8) + n/32768, exact in f32 (one launch)."""
+    import torch
+
+    from app.encoders import gemm_nt
+
+    M, N, K = 128, 4096, 64
+    A = torch.zeros(M, K, dtype=torch.float16, device=cuda)
+    A[:, 0] = torch.arange(M, device=cuda, dtype=torch.float32) / 8 - 8
+    W = torch.zeros(N, K, dtype=torch.float16, device=cuda)
+    W[:, 0] = 1.0
+    bias = torch.arange(N, device=cuda, dtype=torch.float32) / 32768
+    out = torch.empty(M, N, dtype=torch.float16, device=cuda)
+    gemm_nt(A, W, bias, out, 2)  # epilogue 2 = gelu_erf(acc + bias)
+    torch.cuda.synchronize()
+    x = A[:, :1].double() + bias.double()[None, :]
+    ref = torch.nn.functional.gelu(x)
+    err = (out.double() - ref).abs()
+    bound = ref.abs() * 2.0 ** -11 + 2e-6
+    assert bool((err <= bound).all()), float((err - bound).max())
+    neg = x < -3.5
+    record_numerics("gelu_erf_epilogue_sweep", out.float().cpu().numpy()[:1], ref.float().cpu().numpy()[:1],
+                    unit=False, max_abs_err=float(err.max()), max_abs_err_x_below_m3p5=float(err[neg].max()))
