@@ -288,3 +288,25 @@ def test_lane_list_overflow_bound(cuda):
         s, r = ix.search(q, k)
         os_, or_ = flat_cosine_topk(x, np.zeros(n), q, k)
         _check(s, r, os_, or_)
+
+
+def test_k11_matches_restatement(cuda):
+    """K11 (topk_merge_kernel) against oracle.merge.topk_merge on random per-shard lists with
+    duplicated scores across lists, empty slots and k of 1, 10, 300: bit-exact."""
+    import torch
+
+    from app.vector_store import topk_merge
+    from oracle.merge import topk_merge as ref_merge
+
+    rng = np.random.default_rng(90)
+    for nl, nq, k in ((2, 7, 1), (8, 33, 10), (3, 5, 300)):
+        s = np.round(rng.uniform(-1, 1, (nl, nq, k)), 2)  # coarse grid: many exact ties
+        s = -np.sort(-s, axis=2)
+        r = np.stack([rng.permutation(100_000)[: nq * k].reshape(nq, k) + 100_000 * l for l in range(nl)])
+        r[rng.random(r.shape) < 0.1] = -1  # empty slots (shards with fewer matches)
+        s = np.where(r < 0, -np.inf, s)
+        gs, gr, g64 = topk_merge(torch.from_numpy(s).to(cuda), torch.from_numpy(r).to(cuda), k)
+        es, er, e64 = ref_merge(s, r, k)
+        np.testing.assert_array_equal(gr.cpu().numpy(), er)
+        np.testing.assert_array_equal(g64.cpu().numpy(), e64)
+        np.testing.assert_array_equal(gs.cpu().numpy(), es)

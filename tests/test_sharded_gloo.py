@@ -1,8 +1,11 @@
-"""N>1 path on CPU: world_size-2 gloo process group running the product's
-ShardedFlatIndex orchestration (row offsets, all-gather layout [world, nq, k], merge)
-with a CPU stand-in for each rank's local GPU index and a numpy restatement of the
-K11 merge as the checker's merge. The merged result must equal the oracle's exact
-top-k over the whole (unsharded) corpus, ties included."""
+"""N>1 path on CPU: world_size 2 and 4 gloo process groups running the product's
+ShardedFlatIndex (row offsets, the all-gather of (f64 score, int64 row) lists into the
+[world, nq, k] layout K11 consumes, the merge call) with a CPU stand-in for each rank's
+local GPU index (the oracle's exact local top-k — what FlatIndex.search returns, pinned by
+tests/test_knn_gpu.py) and ``oracle.merge.topk_merge``, the documented restatement of K11
+(knn.hip topk_merge_kernel), as the merge. K11 itself is checked against the same
+restatement on the GPU (tests/test_knn_gpu.py::test_k11_matches_restatement). The merged
+result must equal the oracle's exact top-k over the whole (unsharded) corpus, ties included."""
 from __future__ import annotations
 
 import os
@@ -30,17 +33,16 @@ class _OracleShard:
         return torch.from_numpy(s.astype(np.float32)), torch.from_numpy(r), torch.from_numpy(s)
 
 
-def _merge_np(s64, rows, k):
-    s = s64.numpy().transpose(1, 0, 2).reshape(s64.shape[1], -1)
-    r = rows.numpy().transpose(1, 0, 2).reshape(rows.shape[1], -1)
-    out_s = np.full((s.shape[0], k), -np.inf)
-    out_r = np.full((s.shape[0], k), -1, dtype=np.int64)
-    for i in range(s.shape[0]):
-        ok = r[i] >= 0
-        order = np.lexsort((r[i][ok], -s[i][ok]))[:k]
-        out_s[i, :order.size] = s[i][ok][order]
-        out_r[i, :order.size] = r[i][ok][order]
-    return torch.from_numpy(out_s.astype(np.float32)), torch.from_numpy(out_r), torch.from_numpy(out_s)
+def _merge_k11(s64, rows, k):
+    """K11 on the CPU (oracle.merge.topk_merge) behind the torch signature of
+    app.vector_store.topk_merge; asserts the gathered layout is [world, nq, k]."""
+    from oracle.merge import topk_merge
+
+    world = dist.get_world_size()
+    assert s64.dtype == torch.float64 and rows.dtype == torch.int64
+    assert s64.shape[0] == world and s64.shape[2] == k and rows.shape == s64.shape
+    out = topk_merge(s64.numpy(), rows.numpy(), k)
+    return tuple(torch.from_numpy(a) for a in out)
 
 
 def _worker(rank, world, port, X, labels, Q, k, label, ret):
@@ -51,7 +53,7 @@ def _worker(rank, world, port, X, labels, Q, k, label, ret):
 
         bounds = np.linspace(0, len(X), world + 1).astype(int)
         lo, hi = bounds[rank], bounds[rank + 1]
-        idx = ShardedFlatIndex(_OracleShard(X[lo:hi], labels[lo:hi]), row_offset=lo, merge=_merge_np)
+        idx = ShardedFlatIndex(_OracleShard(X[lo:hi], labels[lo:hi]), row_offset=lo, merge=_merge_k11)
         s, r = idx.search(torch.from_numpy(Q), k, label=label)
         ret[rank] = (s.numpy(), r.numpy())
     finally:
@@ -64,8 +66,8 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("label", [-1, 2])
-def test_sharded_equals_unsharded(label):
+@pytest.mark.parametrize("world,label", [(2, -1), (2, 2), (4, -1)])
+def test_sharded_equals_unsharded(world, label):
     from oracle.knn import flat_cosine_topk
 
     X = clustered_corpus(3001, 96, 4, dup_frac=0.3)  # ties across the shard boundary
@@ -73,9 +75,9 @@ def test_sharded_equals_unsharded(label):
     Q = unit_rows(9, 96, 5)
     k = 10
     ret = mp.Manager().dict()
-    mp.spawn(_worker, args=(2, _free_port(), X, labels, Q, k, label, ret), nprocs=2, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), X, labels, Q, k, label, ret), nprocs=world, join=True)
     es, er = flat_cosine_topk(X, labels, Q, k, label_filter=label)
-    for rank in range(2):
+    for rank in range(world):
         s, r = ret[rank]
         np.testing.assert_array_equal(r, er)
         np.testing.assert_allclose(s, es.astype(np.float32), atol=1e-7)
