@@ -145,23 +145,32 @@ def retrieve(user_id: str, query: str) -> List[Dict[str, Any]]:
     return fused
 
 
+def _rerank_pairs(query: str, results: List[Dict[str, Any]]) -> List[Tuple[str, str]]:
+    """The (query, passage) pairs ``_rerank_text`` scores (reference :142-150)."""
+    top = results[: settings.retrieval.rerank_topk]
+    return [(query, item["text"]) for item in top if item.get("text")]
+
+
+def _apply_rerank(results: List[Dict[str, Any]], scores) -> List[Dict[str, Any]]:
+    """Reference :151-155 on precomputed cross-encoder scores (zip with the top items)."""
+    top = results[: settings.retrieval.rerank_topk]
+    for item, score in zip(top, scores):
+        item["rerank_score"] = float(score)
+    reranked = top + results[len(top):]
+    reranked.sort(key=lambda item: item.get("rerank_score", item["score"]), reverse=True)
+    return reranked
+
+
 def _rerank_text(query: str, results: List[Dict[str, Any]]) -> List[Dict[str, Any]]:
     if not results or not settings.retrieval.use_rerank:
         return results
     cross_encoder = _get_cross_encoder()
     if not cross_encoder:
         return results
-    top = results[: settings.retrieval.rerank_topk]
-    if not top:
-        return results
-    pairs = [(query, item["text"]) for item in top if item.get("text")]
+    pairs = _rerank_pairs(query, results)
     if not pairs:
         return results
-    for item, score in zip(top, cross_encoder.predict(pairs)):
-        item["rerank_score"] = float(score)
-    reranked = top + results[len(top):]
-    reranked.sort(key=lambda item: item.get("rerank_score", item["score"]), reverse=True)
-    return reranked
+    return _apply_rerank(results, cross_encoder.predict(pairs))
 
 
 def _z_scores(values: Sequence[Optional[float]]) -> List[float]:

@@ -2,9 +2,10 @@
 
 The reference answers one query per call (``retrieve_text`` / ``retrieve_images``,
 app/ml/retrieve.py:41-100), each a separate scan. These entry points take many
-queries at once: one encoder batch per tower and ONE flat-index launch per modality
-for the whole batch, then the same per-query post-processing and the reference's
-z-score fusion (rerank off). Results for query i equal ``retrieve_text(user, q_i)`` /
+queries at once: one encoder batch per tower, ONE flat-index launch per modality for the
+whole batch, ONE cross-encoder batch for every query's rerank pairs (when rerank is on and
+a reranker loads, as ``retrieve``), then the same per-query post-processing and the
+reference's z-score fusion. Results for query i equal ``retrieve_text(user, q_i)`` /
 ``retrieve_images`` / ``retrieve`` without the cache.
 """
 from __future__ import annotations
@@ -46,8 +47,10 @@ def search_batch(modality: str, user_id: str, query_vecs: np.ndarray, top_k: int
 
 
 def retrieve_batch(user_id: str, queries: Sequence[str], top_k_text: Optional[int] = None,
-                   top_k_image: Optional[int] = None) -> List[List[Dict[str, Any]]]:
-    """Fused text+image results per query (rerank off), batched end to end."""
+                   top_k_image: Optional[int] = None, rerank: Optional[bool] = None) -> List[List[Dict[str, Any]]]:
+    """Fused text+image results per query, batched end to end = ``retrieve(user_id, q)``
+    (app/ml/retrieve.py:103-117) for every q. ``rerank`` defaults to RERANK_ENABLED; the
+    cross-encoder is ``retrieve._get_cross_encoder()`` (False -> no rerank, as retrieve)."""
     from app.ml import retrieve as r
     from app.ml.embeddings import _ensure_clip, _ensure_processor, _normalize, _to_numpy
 
@@ -77,8 +80,19 @@ def retrieve_batch(user_id: str, queries: Sequence[str], top_k_text: Optional[in
             if c:
                 images.append({"chunk_id": c.id, "modality": "image", "score": float(e["score"]),
                                "metadata": r._prepare_metadata(c), "text": None})
-        out.append(r._fuse_results(texts, images))
-    return out
+        out.append((texts, images))
+    use_rr = settings.retrieval.use_rerank if rerank is None else bool(rerank)
+    ce = r._get_cross_encoder() if use_rr else None
+    if ce:
+        pairs, spans = [], []
+        for i, (texts, _) in enumerate(out):
+            p = r._rerank_pairs(qs[i], texts) if texts else []
+            spans.append((len(pairs), len(p)))
+            pairs.extend(p)
+        scores = np.asarray(ce.predict(pairs, batch_size=256)).reshape(-1) if pairs else np.empty(0)
+        out = [(r._apply_rerank(texts, scores[a:a + n]) if n else texts, images)
+               for (texts, images), (a, n) in zip(out, spans)]
+    return [r._fuse_results(texts, images) for texts, images in out]
 
 
 def _z_rows(scores64: np.ndarray, valid: np.ndarray) -> np.ndarray:

@@ -134,10 +134,25 @@ def test_index_retrieve_end_to_end(cuda, tmp_path, monkeypatch):
     clear_all_caches()
     single = [retrieve._fuse_results(retrieve.retrieve_text("alice", q), retrieve.retrieve_images("alice", q))
               for q in queries]
-    batched = retrieve_batch("alice", queries)
+    batched = retrieve_batch("alice", queries)  # RERANK_ENABLED, but no reranker loads offline
     for a, b in zip(single, batched):
         assert [x["chunk_id"] for x in a] == [x["chunk_id"] for x in b]
         assert [x["combined_score"] for x in a] == pytest.approx([x["combined_score"] for x in b], abs=1e-5)
+
+    # with a cross-encoder (GPU, synthetic weights): batched == retrieve() with rerank, the
+    # reference default RERANK_ENABLED=true (app/ml/retrieve.py:103-155)
+    from app.encoders.models import CrossEncoderModel
+
+    monkeypatch.setattr(retrieve, "_CROSS_ENCODER", CrossEncoderModel(synthetic=True))
+    clear_all_caches()
+    single_rr = [retrieve.retrieve("alice", q) for q in queries]
+    reranked = [retrieve._rerank_text(q, retrieve.retrieve_text("alice", q)) for q in queries]
+    assert all("rerank_score" in x for res in reranked for x in res[:8])
+    batched_rr = retrieve_batch("alice", queries, rerank=True)
+    for a, b in zip(single_rr, batched_rr):
+        assert [x["chunk_id"] for x in a] == [x["chunk_id"] for x in b]
+        assert [x["combined_score"] for x in a] == pytest.approx([x["combined_score"] for x in b], abs=1e-5)
+        assert [x.get("rerank_score") for x in a] == pytest.approx([x.get("rerank_score") for x in b], abs=1e-5)
 
 
 def test_store_persists_across_restart(cuda, tmp_path):
