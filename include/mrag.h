@@ -124,6 +124,18 @@ int mrag_topk_merge(const double* scores64, const int64_t* rows, int32_t nlists,
                     int32_t k, float* out_scores, double* out_scores64, int64_t* out_rows,
                     void* stream);
 
+/* ---- K12: z-score fusion of text and image hits ----------------------------
+ * Replaces app/ml/retrieve.py:158-195 (_z_scores + _fuse_results, rerank off) for a batch
+ * of queries, bit-identical to the reference's float32 numpy arithmetic: per query, the
+ * text hit scores text_scores [nq][kt] and image hit scores image_scores [nq][ki] (f32 as
+ * mrag_knn_search returns them, hits in score order, -inf for missing hits; each score is
+ * taken through the store's 1 - f32(1 - s)), z-scored per list, concatenated text-first,
+ * stably sorted by combined score descending. Outputs pick [nq][final_n] (index into the
+ * concatenated [kt | ki] slots, -1 past the hits) and combined [nq][final_n] (f64 z, NaN
+ * for -1). Device pointers; asynchronous on `stream`. */
+int mrag_fuse_scores(const float* text_scores, int32_t kt, const float* image_scores, int32_t ki, int64_t nq,
+                     int32_t final_n, int64_t* pick, double* combined, void* stream);
+
 /* ---- K1..K5: encoders ----------------------------------------------------
  * One handle = one encoder tower on one device:
  *   MRAG_ENC_CLIP_VISION  replaces CLIPModel.get_image_features
@@ -139,7 +151,10 @@ int mrag_topk_merge(const double* scores64, const int64_t* rows, int32_t nlists,
  * Parameters are set by Hugging Face state-dict name (f32 host arrays, e.g.
  * "vision_model.encoder.layers.0.self_attn.q_proj.weight"); compute is fp16 MFMA
  * GEMMs with f32 accumulation and an f32 residual stream. With normalize != 0 the
- * output rows go through K6 (the reference's numpy _normalize, bit-exact). */
+ * output rows go through K6 (the reference's numpy _normalize, bit-exact).
+ * Host pointers (MRAG_PTR_HOST): the call returns with `out` written. Device pointers:
+ * the work is enqueued on `stream` and the call returns without waiting (stream-ordered;
+ * a later call on another stream is ordered after it by the handle). */
 #define MRAG_ENC_CLIP_VISION 1
 #define MRAG_ENC_CLIP_TEXT 2
 #define MRAG_ENC_BERT 3

@@ -42,6 +42,7 @@ SIGNATURES = {
     "mrag_knn_last_stats": (_c_int, [_vp, ctypes.POINTER(_c_i64), ctypes.POINTER(_c_i64)]),
     "mrag_knn_profile": (_c_int, [_vp, _c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_c_i64)]),
     "mrag_topk_merge": (_c_int, [_vp, _vp, _c_int, _c_i64, _c_int, _vp, _vp, _vp, _vp]),
+    "mrag_fuse_scores": (_c_int, [_vp, _c_int, _vp, _c_int, _c_i64, _c_int, _vp, _vp, _vp]),
     "mrag_image_resize_crop": (_c_int, [_vp, ctypes.POINTER(_c_i64), ctypes.POINTER(_c_int),
                                         ctypes.POINTER(_c_int), _c_int, _c_int, _vp, _vp]),
 }

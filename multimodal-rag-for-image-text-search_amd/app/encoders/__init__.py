@@ -240,6 +240,16 @@ def vit_flops_per_image(cfg: EncoderConfig = CLIP_VISION_B32) -> float:
     return float(lin + attn + patch + proj)
 
 
+def text_flops_per_sequence(cfg: EncoderConfig, L: int) -> float:
+    """Algorithmic FLOP of one text-tower forward at sequence length L: the linear layers
+    (q, k, v, out, fc1, fc2), attention (QK^T and PV) and, for CLIP text, the projection."""
+    D, I = cfg.hidden, cfg.intermediate
+    lin = 2 * L * (4 * D * D + 2 * D * I) * cfg.layers
+    attn = 2 * 2 * L * L * D * cfg.layers
+    proj = 2 * D * cfg.proj_dim if cfg.kind == 2 else 0
+    return float(lin + attn + proj)
+
+
 def smoke_encoders() -> None:
     """One small forward of each tower on cuda:0, finite unit rows."""
     rng = np.random.default_rng(0)
@@ -255,4 +265,5 @@ def smoke_encoders() -> None:
 
 
 __all__ = ["GpuEncoder", "load_encoder", "gemm_nt", "bench_clip_images", "smoke_encoders", "CLIP_VISION_B32",
-           "CLIP_TEXT_B32", "MINILM_L6", "EncoderConfig", "param_specs", "vit_flops_per_image"]
+           "CLIP_TEXT_B32", "MINILM_L6", "EncoderConfig", "param_specs", "vit_flops_per_image",
+           "text_flops_per_sequence"]

@@ -150,4 +150,27 @@ def fuse_scores(text_scores, image_scores, final_n: Optional[int] = None):
     return pick, combined
 
 
-__all__ = ["search_batch", "retrieve_batch", "fuse_scores"]
+def fuse_scores_gpu(text_scores, image_scores, final_n: Optional[int] = None):
+    """``fuse_scores`` on the GPU (K12, ``mrag_fuse_scores``): torch CUDA f32 ``[Q, kt]`` /
+    ``[Q, ki]`` hit scores (as ``FlatIndex.search`` returns them) -> (``pick`` int64 CUDA
+    ``[Q, final_n]``, ``combined`` f64 CUDA ``[Q, final_n]``), bit-identical to ``fuse_scores``
+    and asynchronous on torch's current stream."""
+    import torch
+
+    from app import _native
+
+    n_final = int(final_n or settings.retrieval.final_n)
+    ts = text_scores.detach().to(torch.float32).contiguous()
+    im = image_scores.detach().to(torch.float32).contiguous()
+    if ts.ndim != 2 or im.ndim != 2 or ts.shape[0] != im.shape[0] or ts.device != im.device:
+        raise ValueError("expected [Q, kt] and [Q, ki] CUDA score tensors on one device")
+    q = ts.shape[0]
+    pick = torch.empty((q, n_final), dtype=torch.int64, device=ts.device)
+    comb = torch.empty((q, n_final), dtype=torch.float64, device=ts.device)
+    stream = torch.cuda.current_stream(ts.device).cuda_stream
+    _native.call("mrag_fuse_scores", ts.data_ptr(), ts.shape[1], im.data_ptr(), im.shape[1], q, n_final,
+                 pick.data_ptr(), comb.data_ptr(), stream)
+    return pick, comb
+
+
+__all__ = ["search_batch", "retrieve_batch", "fuse_scores", "fuse_scores_gpu"]

@@ -70,6 +70,12 @@ struct mrag_encoder {
   // workspace
   Buf X, H16, QKV, ATT, F16, PATCH, IMG, IDS, MASK, TYPES, ROWS, POOL16, OUT;
   int64_t ws_tokens = 0;
+  // Device-pointer calls return without a host sync (stream-ordered, like any kernel launch):
+  // `done` marks the end of the last call's work on `last_stream`; a call on another stream
+  // first waits for it (the workspace is shared), and a workspace reallocation first
+  // drains it.
+  hipEvent_t done = nullptr;
+  hipStream_t last_stream = nullptr;
 };
 
 namespace {
@@ -217,6 +223,7 @@ int layer_index(const std::string& name, const std::string& marker) {
 int ensure_workspace(mrag_encoder* e, int B, int T) {
   const int64_t tokens = (int64_t)B * T;
   if (tokens <= e->ws_tokens) return MRAG_OK;
+  if (e->last_stream) MRAG_HIP(hipEventSynchronize(e->done));  // in-flight work still reads the old buffers
   const auto& c = e->cfg;
   const int64_t D = c.hidden, I = c.intermediate;
   if (int rc = buf_ensure(e->X, tokens * D * 4)) return rc;
@@ -362,6 +369,7 @@ int mrag_encoder_create(const mrag_encoder_config* cfg, int32_t device, mrag_enc
   e->layers.resize(c.layers);
   e->expected = expected_names(c);
   hipError_t err = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
+  if (err == hipSuccess) err = hipEventCreateWithFlags(&e->done, hipEventDisableTiming);
   if (err != hipSuccess) {
     delete e;
     return mrag::fail(MRAG_ERR_HIP, "stream: %s", hipGetErrorString(err));
@@ -375,6 +383,8 @@ int mrag_encoder_destroy(mrag_encoder* e) {
   {
     mrag::DeviceGuard g(e->device);
     (void)hipStreamSynchronize(e->stream);
+    if (e->last_stream) (void)hipEventSynchronize(e->done);
+    if (e->done) (void)hipEventDestroy(e->done);
     for (auto& L : e->layers)
       for (Buf* b : {&L.wqkv, &L.bqkv, &L.wo, &L.bo, &L.w1, &L.b1, &L.w2, &L.b2, &L.ln1g, &L.ln1b, &L.ln2g, &L.ln2b})
         buf_free(*b);
@@ -393,6 +403,7 @@ int mrag_encoder_set_param(mrag_encoder* e, const char* cname, const float* data
   MRAG_REQUIRE(e && cname && data, "NULL argument");
   std::lock_guard<std::mutex> lk(e->mu);
   mrag::DeviceGuard g(e->device);
+  if (e->last_stream) MRAG_HIP(hipEventSynchronize(e->done));  // a forward may still read the weights
   const std::string name(cname);
   const auto& c = e->cfg;
   bool known = false;
@@ -485,6 +496,21 @@ int mrag_encoder_missing(const mrag_encoder* e, int64_t* count) {
   return MRAG_OK;
 }
 
+// Start of a forward on stream s: order it after the previous call if that ran elsewhere.
+int begin_call(mrag_encoder* e, hipStream_t s) {
+  if (e->last_stream && e->last_stream != s) MRAG_HIP(hipStreamWaitEvent(s, e->done, 0));
+  return MRAG_OK;
+}
+
+// End of a forward: host pointers are complete on return (synchronous copy-out); device
+// pointers are stream-ordered (no host sync).
+int end_call(mrag_encoder* e, hipStream_t s, int32_t ptr_kind) {
+  MRAG_HIP(hipEventRecord(e->done, s));
+  e->last_stream = s;
+  if (ptr_kind == MRAG_PTR_HOST) MRAG_HIP(hipStreamSynchronize(s));
+  return MRAG_OK;
+}
+
 int mrag_encoder_embed_images(mrag_encoder* e, const uint8_t* images, int32_t batch, float* out, int32_t normalize,
                               int32_t ptr_kind, void* stream_arg) {
   MRAG_REQUIRE(e != nullptr, "NULL encoder");
@@ -497,6 +523,7 @@ int mrag_encoder_embed_images(mrag_encoder* e, const uint8_t* images, int32_t ba
   if (batch == 0) return MRAG_OK;
   MRAG_REQUIRE(images && out, "NULL images/out");
   hipStream_t s = stream_arg ? (hipStream_t)stream_arg : e->stream;
+  if (int rc = begin_call(e, s)) return rc;
   const auto& c = e->cfg;
   const int S = c.image_size, P = c.patch_size, G = S / P, T = G * G + 1, D = c.hidden, B = batch;
   const int Kp = 3 * P * P;
@@ -529,8 +556,7 @@ int mrag_encoder_embed_images(mrag_encoder* e, const uint8_t* images, int32_t ba
     if (int rc = mrag_l2norm_rows(dst, dst, B, c.proj_dim, s)) return rc;
   if (ptr_kind == MRAG_PTR_HOST)
     MRAG_HIP(hipMemcpyAsync(out, dst, (size_t)B * c.proj_dim * 4, hipMemcpyDeviceToHost, s));
-  MRAG_HIP(hipStreamSynchronize(s));
-  return MRAG_OK;
+  return end_call(e, s, ptr_kind);
 }
 
 int mrag_encoder_embed_tokens(mrag_encoder* e, const int32_t* ids, const int32_t* mask, int32_t batch, int32_t seq,
@@ -547,6 +573,7 @@ int mrag_encoder_embed_tokens(mrag_encoder* e, const int32_t* ids, const int32_t
   if (batch == 0) return MRAG_OK;
   MRAG_REQUIRE(ids && out, "NULL ids/out");
   hipStream_t s = stream_arg ? (hipStream_t)stream_arg : e->stream;
+  if (int rc = begin_call(e, s)) return rc;
   const auto& c = e->cfg;
   const int B = batch, T = seq, D = c.hidden;
   if (int rc = ensure_workspace(e, B, T)) return rc;
@@ -593,8 +620,7 @@ int mrag_encoder_embed_tokens(mrag_encoder* e, const int32_t* ids, const int32_t
   if (normalize)
     if (int rc = mrag_l2norm_rows(dst, dst, B, outD, s)) return rc;
   if (ptr_kind == MRAG_PTR_HOST) MRAG_HIP(hipMemcpyAsync(out, dst, (size_t)B * outD * 4, hipMemcpyDeviceToHost, s));
-  MRAG_HIP(hipStreamSynchronize(s));
-  return MRAG_OK;
+  return end_call(e, s, ptr_kind);
 }
 
 int mrag_encoder_score_pairs(mrag_encoder* e, const int32_t* ids, const int32_t* type_ids, const int32_t* mask,
@@ -611,6 +637,7 @@ int mrag_encoder_score_pairs(mrag_encoder* e, const int32_t* ids, const int32_t*
   if (batch == 0) return MRAG_OK;
   MRAG_REQUIRE(ids && out, "NULL ids/out");
   hipStream_t s = stream_arg ? (hipStream_t)stream_arg : e->stream;
+  if (int rc = begin_call(e, s)) return rc;
   const auto& c = e->cfg;
   const int B = batch, T = seq, D = c.hidden, NL = c.proj_dim;
   if (int rc = ensure_workspace(e, B, T)) return rc;
@@ -662,8 +689,7 @@ int mrag_encoder_score_pairs(mrag_encoder* e, const int32_t* ids, const int32_t*
                                NL, s))
     return rc;
   if (ptr_kind == MRAG_PTR_HOST) MRAG_HIP(hipMemcpyAsync(out, dst, (size_t)B * NL * 4, hipMemcpyDeviceToHost, s));
-  MRAG_HIP(hipStreamSynchronize(s));
-  return MRAG_OK;
+  return end_call(e, s, ptr_kind);
 }
 
 int mrag_gemm_nt(const void* A, const void* W, const float* bias, void* C, int32_t M, int32_t N, int32_t K,

@@ -125,6 +125,11 @@ def test_config5_fusion_leg(cuda):
     st, rt = indexes[0].search(tv, kt)
     si, ri = indexes[1].search(iv, ki)
     pick, comb = fuse_scores(st.cpu().numpy(), si.cpu().numpy(), final_n)
+    from app.retrieval import fuse_scores_gpu
+
+    gpick, gcomb = fuse_scores_gpu(st, si, final_n)  # K12, what the bench leg runs
+    np.testing.assert_array_equal(gpick.cpu().numpy(), pick)
+    np.testing.assert_array_equal(gcomb.cpu().numpy(), comb)
 
     sel = np.arange(0, nq, 4)  # 250 of the 1000 queries against the f64 oracle
     tvh, ivh = tv.cpu().numpy(), iv.cpu().numpy()
