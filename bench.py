@@ -145,12 +145,13 @@ def cpu_baseline(seconds_budget: float = 20.0):
     r_np, t_np = _median_rate(lambda: np_search(q[:nb]), nb)
     r_t, t_t = _median_rate(lambda: torch_search(q[:nb]), nb)
     best = max(r_np, r_t)
+    info = _host_info()
     return {
         "value": round(best, 2),
         "unit": "queries/s (1M x 512 f32 corpus, top-10)",
-        "cores": _host_info()["affinity_cores"],
+        "cores": info["torch_threads"] if r_t >= r_np else (info["blas_threads"] or info["affinity_cores"]),
+        "host": info,
         "kind": "port",
-        "host": _host_info(),
         "variants_queries_per_s": {"numpy_matmul_argpartition": round(r_np, 2), "torch_mm_topk": round(r_t, 2)},
         "sample": f"{nb} of the 1000 queries against the same 1M x 512 corpus shape (f32, unit rows), median of 5 "
                   f"timed batches per variant (numpy {np.median(t_np):.2f} s, torch {np.median(t_t):.2f} s per batch); "
@@ -273,7 +274,7 @@ def fusion_cpu_baseline(seconds_budget: float = 20.0):
     nb = int(min(256, max(8, seconds_budget / 6 / max(per, 1e-5))))
     rate, ts = _median_rate(lambda: run(nb), nb)
     return {"value": round(rate, 2), "unit": "queries/s (one GPU's shard: 2^19 x 384 text + 2^19 x 512 image rows)",
-            "cores": _host_info()["affinity_cores"], "kind": "port", "host": _host_info(),
+            "cores": int(torch.get_num_threads()), "kind": "port", "host": _host_info(),
             "sample": f"{nb} synthetic {FUSION_T}-token queries: transformers MiniLM + CLIP-text fp32, torch mm + topk "
                       f"(k={kt}/{ki}) over the two corpora, oracle.fusion per query; median of 5 "
                       f"({ts[len(ts) // 2]:.2f} s per batch)"}
@@ -335,17 +336,22 @@ def fusion_leg(world: int, rank: int, local: int, steps: int, warmup: int):
             return pick.cpu()
         return None
 
-    for _ in range(warmup):
-        step()
+    # the leg runs on its own stream: device-pointer encoder calls are then stream-ordered
+    # (no host sync per call; on the default stream the library synchronises every call)
+    leg_stream = torch.cuda.Stream(device=dev)
     torch.cuda.synchronize()
-    _barrier(world)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        pick = step()
-    torch.cuda.synchronize()
-    _barrier(world)
-    dt = _max_over_ranks(time.perf_counter() - t0, world)
+    with torch.cuda.stream(leg_stream):
+        for _ in range(warmup):
+            step()
+        torch.cuda.synchronize()
+        _barrier(world)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            pick = step()
+        torch.cuda.synchronize()
+        _barrier(world)
+        dt = _max_over_ranks(time.perf_counter() - t0, world)
     if rank != 0:
         return None
     fl = fusion_flops_per_query(world)

@@ -152,9 +152,10 @@ int mrag_fuse_scores(const float* text_scores, int32_t kt, const float* image_sc
  * "vision_model.encoder.layers.0.self_attn.q_proj.weight"); compute is fp16 MFMA
  * GEMMs with f32 accumulation and an f32 residual stream. With normalize != 0 the
  * output rows go through K6 (the reference's numpy _normalize, bit-exact).
- * Host pointers (MRAG_PTR_HOST): the call returns with `out` written. Device pointers:
- * the work is enqueued on `stream` and the call returns without waiting (stream-ordered;
- * a later call on another stream is ordered after it by the handle). */
+ * Host pointers (MRAG_PTR_HOST), or stream == NULL (the handle's own stream): the call
+ * returns with `out` written. Device pointers on a caller stream: the work is enqueued on
+ * `stream` and the call returns without waiting (stream-ordered; a later call on another
+ * stream is ordered after it by the handle). */
 #define MRAG_ENC_CLIP_VISION 1
 #define MRAG_ENC_CLIP_TEXT 2
 #define MRAG_ENC_BERT 3

@@ -147,6 +147,10 @@ def fuse_scores(text_scores, image_scores, final_n: Optional[int] = None):
     order = np.argsort(key, axis=1, kind="stable")[:, :n_final]
     pick = np.where(np.take_along_axis(valid, order, axis=1), order, -1).astype(np.int64)
     combined = np.where(pick >= 0, np.take_along_axis(comb, order, axis=1), np.nan)
+    if pick.shape[1] < n_final:  # fewer slots than final_n: pad ([Q, final_n] like K12)
+        pad = n_final - pick.shape[1]
+        pick = np.pad(pick, ((0, 0), (0, pad)), constant_values=-1)
+        combined = np.pad(combined, ((0, 0), (0, pad)), constant_values=np.nan)
     return pick, combined
 
 

@@ -502,12 +502,13 @@ int begin_call(mrag_encoder* e, hipStream_t s) {
   return MRAG_OK;
 }
 
-// End of a forward: host pointers are complete on return (synchronous copy-out); device
-// pointers are stream-ordered (no host sync).
-int end_call(mrag_encoder* e, hipStream_t s, int32_t ptr_kind) {
+// End of a forward: host pointers, or no caller stream (NULL = the handle's own stream, which
+// the caller cannot order on), are complete on return; device pointers on a caller stream are
+// stream-ordered (no host sync).
+int end_call(mrag_encoder* e, hipStream_t s, int32_t ptr_kind, void* stream_arg) {
   MRAG_HIP(hipEventRecord(e->done, s));
   e->last_stream = s;
-  if (ptr_kind == MRAG_PTR_HOST) MRAG_HIP(hipStreamSynchronize(s));
+  if (ptr_kind == MRAG_PTR_HOST || stream_arg == nullptr) MRAG_HIP(hipStreamSynchronize(s));
   return MRAG_OK;
 }
 
@@ -556,7 +557,7 @@ int mrag_encoder_embed_images(mrag_encoder* e, const uint8_t* images, int32_t ba
     if (int rc = mrag_l2norm_rows(dst, dst, B, c.proj_dim, s)) return rc;
   if (ptr_kind == MRAG_PTR_HOST)
     MRAG_HIP(hipMemcpyAsync(out, dst, (size_t)B * c.proj_dim * 4, hipMemcpyDeviceToHost, s));
-  return end_call(e, s, ptr_kind);
+  return end_call(e, s, ptr_kind, stream_arg);
 }
 
 int mrag_encoder_embed_tokens(mrag_encoder* e, const int32_t* ids, const int32_t* mask, int32_t batch, int32_t seq,
@@ -620,7 +621,7 @@ int mrag_encoder_embed_tokens(mrag_encoder* e, const int32_t* ids, const int32_t
   if (normalize)
     if (int rc = mrag_l2norm_rows(dst, dst, B, outD, s)) return rc;
   if (ptr_kind == MRAG_PTR_HOST) MRAG_HIP(hipMemcpyAsync(out, dst, (size_t)B * outD * 4, hipMemcpyDeviceToHost, s));
-  return end_call(e, s, ptr_kind);
+  return end_call(e, s, ptr_kind, stream_arg);
 }
 
 int mrag_encoder_score_pairs(mrag_encoder* e, const int32_t* ids, const int32_t* type_ids, const int32_t* mask,
@@ -689,7 +690,7 @@ int mrag_encoder_score_pairs(mrag_encoder* e, const int32_t* ids, const int32_t*
                                NL, s))
     return rc;
   if (ptr_kind == MRAG_PTR_HOST) MRAG_HIP(hipMemcpyAsync(out, dst, (size_t)B * NL * 4, hipMemcpyDeviceToHost, s));
-  return end_call(e, s, ptr_kind);
+  return end_call(e, s, ptr_kind, stream_arg);
 }
 
 int mrag_gemm_nt(const void* A, const void* W, const float* bias, void* C, int32_t M, int32_t N, int32_t K,

@@ -212,12 +212,15 @@ print("ok")
     res = subprocess.run([sys.executable, "-c", code, os.path.join(root, "multimodal-rag-for-image-text-search_amd"),
                           root, db], capture_output=True, text=True, timeout=240)
     assert res.returncode == 0 and "ok" in res.stdout, res.stderr[-2000:]
-    stored = np.asarray([store_normalize(x) for x in X], np.float32)
-    stored[7] = store_normalize(X[399])
-    lab = np.zeros(400, np.int64)
+    # store rows in commit order: c0..c399, then c7's new row (row 400; row 7 tombstoned) —
+    # c7 now ties exactly with c399 and ranks after it (row asc)
+    stored = np.asarray([store_normalize(x) for x in np.concatenate([X, X[399:400]])], np.float32)
+    names = [f"c{i}" for i in range(400)] + ["c7"]
+    lab = np.zeros(401, np.int64)
+    lab[7] = -2
     os_, or_ = flat_cosine_topk(stored, lab, np.asarray([store_normalize(q)], np.float32), 400)
     got = store.search_text("alice", q, 400)
-    assert [g["chunk_id"] for g in got] == [f"c{r}" for r in or_[0] if r >= 0]
+    assert [g["chunk_id"] for g in got] == [names[r] for r in or_[0] if r >= 0]
     assert len(got) == 400 and [g for g in got if g["chunk_id"] == "c7"][0]["meta"] == {"i": "moved"}
     store.upsert_text_vectors([ls.VectorRow("c8", "alice", "d", "text", X[0], {"i": "mine"})])
     got = store.search_text("alice", X[0], 2)
