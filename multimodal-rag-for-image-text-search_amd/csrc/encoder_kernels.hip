@@ -1021,6 +1021,117 @@ __global__ __launch_bounds__(256) void attention_mfma64t_kernel(AttentionArgs a)
   }
 }
 
+// K4 v3 (flash form, any L <= 512, head_dim 32 or 64): one wave per (sequence, head, 16-query
+// block); key blocks of 16 with an online softmax, all on MFMA 16x16:
+//   S^T = K . Q^T    (16x16x32, DH/32 k-steps): lane (c, g) = (l & 15, l >> 4) holds query
+//                    16 qb + c and keys 16 kb + 4 g + r — the query's row max / sum are the lane's
+//                    4 registers plus two xor shuffles (16, 32);
+//   O^T += V^T . P^T (16x16x16, one per 16 dims): P^T is the S^T accumulator cast to f16 in place
+//                    (B operand: keys 4 g .. 4 g + 3 of query c), V^T comes from the wave's LDS
+//                    copy of the key block by ds_read_b64_tr_b16 (A operand: dim 16 db + c, the
+//                    same 4 keys); O^T holds 4 consecutive dims of query c: one 8-byte store each.
+// Key blocks whose keys are all masked (the padding of a shorter sequence in a longer batch)
+// are skipped, and every other block is processed identically whatever the batch's length:
+// a sequence's result does not depend on how its batch is padded, for every L. Work per
+// (sequence, head) grows with its own length only, not with a 64-row pad.
+template <int DH>
+__global__ __launch_bounds__(256) void attention_flash16_kernel(AttentionArgs a) {
+  constexpr int KS = DH / 32;               // 32-dim k-steps of S^T
+  constexpr int DB = DH / 16;               // 16-dim blocks of O^T
+  constexpr int VROW = DH == 64 ? 96 : 48;  // LDS row stride (halves): a transposed read's 4 rows hit disjoint banks
+  typedef _Float16 half4_v __attribute__((ext_vector_type(4)));
+  __shared__ __attribute__((aligned(16))) _Float16 Vs[4][16 * VROW];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = lane & 15, g = lane >> 4;
+  const int L = a.L, nqb = (L + 15) >> 4;
+  const int item = blockIdx.x * 4 + w;
+  if (item >= a.B * a.H * nqb) return;  // whole wave (the transposed reads need EXEC all ones)
+  const int qb = item % nqb, bh = item / nqb;
+  const int hd = bh % a.H, b = bh / a.H;
+  const int D = a.H * DH;
+  const size_t rs = (size_t)3 * D;
+  const _Float16* base = a.qkv + (size_t)b * L * rs + hd * DH;
+  const int qrow = 16 * qb + c;
+  half8 qf[KS];
+#pragma unroll
+  for (int st = 0; st < KS; ++st)
+    qf[st] = qrow < L ? *(const half8*)(base + (size_t)qrow * rs + 32 * st + 8 * g) : half8{};
+  f32x4 o[DB];
+#pragma unroll
+  for (int db = 0; db < DB; ++db) o[db] = f32x4{};
+  float m = -INFINITY, l = 0.f;
+  _Float16* vs = Vs[w];
+  const int nkb = a.causal ? min((L + 15) >> 4, qb + 1) : (L + 15) >> 4;
+  for (int kb = 0; kb < nkb; ++kb) {
+    bool kv[4];
+    bool any_ok = false;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int key = 16 * kb + 4 * g + r;
+      bool ok = key < L;
+      if (ok && a.mask) ok = a.mask[(size_t)b * L + key] != 0;
+      if (a.causal) ok = ok && key <= qrow;
+      kv[r] = ok;
+      any_ok |= ok;
+    }
+    if (!__any(any_ok)) continue;  // wave-uniform
+    const int krow = 16 * kb + c;
+    f32x4 sacc = {};
+#pragma unroll
+    for (int st = 0; st < KS; ++st) {
+      const half8 kf = krow < L ? *(const half8*)(base + (size_t)krow * rs + D + 32 * st + 8 * g) : half8{};
+      sacc = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf, qf[st], sacc, 0, 0, 0);
+    }
+    // V rows of the block -> this wave's LDS image (16 B per lane per row chunk)
+    asm volatile("" ::: "memory");  // the previous block's transposed reads come first
+#pragma unroll
+    for (int t = 0; t < KS; ++t) {
+      const int idx = lane + 64 * t, key = idx / (DH / 8), ch = idx % (DH / 8);
+      const int kr = 16 * kb + key;
+      const half8 v = kr < L ? *(const half8*)(base + (size_t)kr * rs + 2 * D + 8 * ch) : half8{};
+      *(half8*)(vs + key * VROW + 8 * ch) = v;
+    }
+    float sv[4], bmax = -INFINITY;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      sv[r] = kv[r] ? sacc[r] * a.scale : -INFINITY;
+      bmax = fmaxf(bmax, sv[r]);
+    }
+    bmax = fmaxf(bmax, __shfl_xor(bmax, 16));
+    bmax = fmaxf(bmax, __shfl_xor(bmax, 32));
+    const float mn = fmaxf(m, bmax);
+    const float alpha = m == -INFINITY ? 0.f : __expf(m - mn);
+    half4_v pf;
+    float ps = 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float pv = sv[r] == -INFINITY ? 0.f : __expf(sv[r] - mn);
+      pf[r] = (_Float16)pv;
+      ps += pv;
+    }
+    ps += __shfl_xor(ps, 16);
+    ps += __shfl_xor(ps, 32);
+    l = l * alpha + ps;
+    m = mn;
+#pragma unroll
+    for (int db = 0; db < DB; ++db) {
+      o[db] *= alpha;
+      const half4_t vt = lds_read_tr16(vs + (4 * g + (c >> 2)) * VROW + 16 * db + 4 * (c & 3));
+      o[db] = __builtin_amdgcn_mfma_f32_16x16x16f16(vt, pf, o[db], 0, 0, 0);
+    }
+  }
+  if (qrow < L) {
+    const float inv = l > 0.f ? 1.f / l : 0.f;
+    _Float16* orow = a.out + ((size_t)b * L + qrow) * D + hd * DH + 4 * g;
+#pragma unroll
+    for (int db = 0; db < DB; ++db) {
+      const half4_t h = {(_Float16)(o[db][0] * inv), (_Float16)(o[db][1] * inv), (_Float16)(o[db][2] * inv),
+                         (_Float16)(o[db][3] * inv)};
+      *(half4_t*)(orow + 16 * db) = h;
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // K1 (prologue): CLIP pixel normalisation fused into the patch im2col.
 // Reference: CLIPImageProcessor rescale (u8 -> f64 * 1/255 -> f32) then (x - mean) / std
@@ -1348,7 +1459,19 @@ int launch_attention(const AttentionArgs& a, int dh, hipStream_t s) {
     const char* e = getenv("MRAG_ATTN_V1");
     return e && atoi(e) == 1;
   }();
-  if (dh == 64 && a.L <= 64 && !force_valu_attention() && !attn_v1) {
+  static const bool legacy = [] {  // MRAG_ATTN_LEGACY=1: the round-1 dispatch (A/B timing)
+    const char* e = getenv("MRAG_ATTN_LEGACY");
+    return e && atoi(e) == 1;
+  }();
+  if ((dh == 64 || dh == 32) && !legacy && !force_valu_attention()) {
+    const int64_t items = (int64_t)a.B * a.H * ((a.L + 15) / 16);
+    MRAG_REQUIRE(items < (1ll << 33), "attention: batch too large");
+    const dim3 g4((unsigned)((items + 3) / 4));
+    if (dh == 64)
+      hipLaunchKernelGGL(attention_flash16_kernel<64>, g4, dim3(256), 0, s, a);
+    else
+      hipLaunchKernelGGL(attention_flash16_kernel<32>, g4, dim3(256), 0, s, a);
+  } else if (dh == 64 && a.L <= 64 && !force_valu_attention() && !attn_v1) {
     hipLaunchKernelGGL(attention_mfma64t_kernel<64>, dim3((unsigned)((a.B * a.H + 3) / 4)), dim3(256), 0, s, a);
   } else if (dh == 32 && a.L <= 64 && mfma_attention_dh32()) {
     // opt-in (MRAG_ATTN_DH32=1): the BERT towers otherwise stay on the f32 VALU kernel for every

@@ -225,3 +225,33 @@ def test_gelu_erf_epilogue_sweep(cuda):
     neg = x < -3.5
     record_numerics("gelu_erf_epilogue_sweep", out.float().cpu().numpy()[:1], ref.float().cpu().numpy()[:1],
                     unit=False, max_abs_err=float(err.max()), max_abs_err_x_below_m3p5=float(err[neg].max()))
+
+
+@pytest.mark.parametrize("tower", ["minilm", "clip_text"])
+def test_padding_invariance(cuda, tower):
+    """A sequence's embedding does not depend on how far its batch is padded (K4 v3 skips fully
+    masked key blocks; every other block, GEMM row, LayerNorm row and the pooling are
+    per-sequence): each sequence alone == the same sequence inside a batch padded to the
+    longest, bit for bit, for lengths across the 16-key block boundaries and past 64."""
+    from app.encoders import CLIP_TEXT_B32, MINILM_L6, GpuEncoder
+
+    cfg = MINILM_L6 if tower == "minilm" else CLIP_TEXT_B32
+    lens = [3, 16, 17, 40, 64, 65, 77] + ([130, 256] if tower == "minilm" else [])
+    T = max(lens)
+    rng = np.random.default_rng(17)
+    ids = np.zeros((len(lens), T), np.int32)
+    mask = np.zeros((len(lens), T), np.int32)
+    for i, n in enumerate(lens):
+        if tower == "minilm":
+            ids[i, :n] = rng.integers(1000, 30000, n)
+            ids[i, 0], ids[i, n - 1] = 101, 102
+        else:
+            ids[i, :n] = rng.integers(1, 49405, n)
+            ids[i, 0], ids[i, n - 1] = 49406, 49407
+            ids[i, n:] = 49407  # CLIP pads with the EOS id (first EOS pooling)
+        mask[i, :n] = 1
+    enc = GpuEncoder(cfg)
+    batch = enc.embed_tokens(ids, mask)
+    for i, n in enumerate(lens):
+        alone = enc.embed_tokens(ids[i:i + 1, :n], mask[i:i + 1, :n])
+        np.testing.assert_array_equal(alone[0], batch[i], err_msg=f"length {n}")
