@@ -1032,6 +1032,267 @@ __global__ __launch_bounds__(SCAN2_THREADS) void knn_scan3_kernel(ScanParams p) 
   }
 }
 
+// ---------------------------------------------------------------------------
+// K7 v4 (top-k mode and sample pre-pass; same lists, part_tau and outputs as v3): two waves per
+// SIMD instead of one, so one wave's MFMAs cover its sibling's LDS-DMA issue, end-of-tile
+// waits, barriers and filter work.
+//  * one workgroup = 8 waves = 256 queries x one split; a wave owns 32 queries as two 16-query
+//    blocks whose B fragments (DP/4 registers: 128 AGPRs at DP = 512) stay in AGPRs, leaving
+//    the other half of a 256-register wave for single-buffered accumulators, one A-fragment
+//    set and the lane lists (KL3 = 6, as v3);
+//  * a 64-row tile is processed in two phases of KSTEPS/2 k-steps (8 MFMA 16x16x32 per k-step:
+//    4 row blocks x 2 query blocks), each phase ended by a raw s_barrier; waves 4..7 (group B,
+//    one per SIMD beside a wave of group A) run one barrier behind waves 0..3, so the two waves
+//    of a SIMD are always in different phases;
+//  * next-tile LDS-DMA: group B issues its pieces in phase 0 of tile t, group A in phase 1 (one
+//    per k-step), each group retiring its own with vmcnt(0) before the barrier that ends the
+//    issuing phase. With the one-barrier stagger, every wave has finished tile t - 1 (whose
+//    buffer is being refilled) before either group's issue phase starts, and every piece of
+//    tile t + 1 has landed at a barrier each wave passes before its first read of it;
+//  * the tile's group tests / list insertions run after the phase-1 MFMAs, while the sibling
+//    wave is in the middle of its own phase.
+constexpr int SCAN4_WAVES = 8;
+constexpr int SCAN4_THREADS = SCAN4_WAVES * 64;
+constexpr int QPW4 = 32;
+static_assert(SCAN4_WAVES * QPW4 == QPG, "v4 keeps the query-group size of v1");
+
+__device__ __forceinline__ void mfma16_guard8(f32x4 (&acc)[4][2]) {
+  asm volatile("s_nop 15\n\ts_nop 3"
+               : "+v"(acc[0][0]), "+v"(acc[0][1]), "+v"(acc[1][0]), "+v"(acc[1][1]), "+v"(acc[2][0]),
+                 "+v"(acc[2][1]), "+v"(acc[3][0]), "+v"(acc[3][1]));
+}
+
+template <int DP, int MODE = 0, int PPK = 4>  // PPK: DMA pieces per k-step, front-loaded in the issue phase
+__global__ __launch_bounds__(SCAN4_THREADS) void knn_scan4_kernel(ScanParams p) {
+  constexpr int KSTEPS = DP / 32;
+  constexpr int HALF = KSTEPS / 2;
+  constexpr int ROW_BYTES = DP * 2;
+  constexpr int TILE_BYTES = TILE_ROWS * ROW_BYTES;
+  constexpr int CPR = DP / 8;
+  constexpr int PIECES = TILE_BYTES / 1024 / SCAN4_WAVES;  // per wave per tile (DP / 64)
+  static_assert(KSTEPS % 2 == 0 && PIECES <= HALF * PPK && PPK <= 4, "the issue phase holds every DMA piece");
+  static_assert(CPR % 16 == 0, "swizzle needs rows of a multiple of 16 chunks");
+  constexpr int LBL_OFF = 2 * TILE_BYTES;
+  __shared__ __attribute__((aligned(16))) char smem[2 * TILE_BYTES + 2 * TILE_ROWS * 4];
+
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int grp = w >> 2;  // 0: waves 0..3 (group A), 1: waves 4..7 (group B, one barrier behind)
+  const int g4 = lane >> 4;
+  const int c16 = lane & 15;
+  const uint32_t lds_base = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)((AS3 char*)smem));
+
+  int qg, split;  // same XCD-aware block mapping as v1..v3
+  {
+    const int b = blockIdx.x;
+    if ((p.splits & 7) == 0) {
+      const int xcd = b & 7, sl = b >> 3;
+      qg = sl % p.qgroups;
+      split = (sl / p.qgroups) * 8 + xcd;
+    } else {
+      qg = b % p.qgroups;
+      split = b / p.qgroups;
+    }
+  }
+  const int slot0 = qg * QPG + w * QPW4 + c16;  // query block qb: slot0 + 16 qb
+
+  half8 qf[KSTEPS][2];
+#pragma unroll
+  for (int kk = 0; kk < KSTEPS; ++kk)
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb)
+      qf[kk][qb] = *(const half8*)(p.q16 + (size_t)(slot0 + 16 * qb) * DP + kk * 32 + g4 * 8);
+#pragma unroll
+  for (int kk = 0; kk < KSTEPS; ++kk) asm volatile("" ::"a"(qf[kk][0]), "a"(qf[kk][1]));
+
+  float ls[2][KL3];
+  int li[2][KL3];
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+    for (int j = 0; j < KL3; ++j) {
+      ls[qb][j] = -INFINITY;
+      li[qb][j] = -1;
+    }
+  float theta_f[2] = {-INFINITY, -INFINITY};
+  uint32_t theta_next[2] = {0u, 0u};
+  float published[2] = {-INFINITY, -INFINITY};
+  float smax[2] = {-INFINITY, -INFINITY};
+  uint32_t* const theta_q = p.theta + slot0;
+  const bool may_publish = p.k <= KL3;
+  const int offA0 = c16 * ROW_BYTES + 16 * (g4 ^ c16);
+
+  int my_tiles = (split < p.ntiles) ? (p.ntiles - 1 - split) / p.splits + 1 : 0;
+  int tstep = p.splits;
+  if constexpr (MODE == 1) {
+    my_tiles = min(my_tiles, p.sample_tiles);
+    tstep = p.splits * p.sample_stride;
+  }
+  if (my_tiles == 0) return;  // whole workgroup, before any barrier
+
+  auto stage_piece = [&](int buf, int tile, int i) {
+    const char* gt = (const char*)p.x16 + (size_t)tile * TILE_BYTES;
+    const unsigned piece = w * PIECES + i;
+    const unsigned P = piece * 64 + (unsigned)lane;
+    const unsigned row = P / CPR;
+    const unsigned pos = P - row * CPR;
+    const unsigned c = pos ^ (row & 15);
+    glds_x4(gt + row * ROW_BYTES + c * 16, lds_base + buf * TILE_BYTES + piece * 1024);
+  };
+  auto bar = [&]() {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  // prologue: tile 0 by every wave, landed before anyone reads it
+#pragma unroll
+  for (int i = 0; i < PIECES; ++i) stage_piece(0, split, i);
+  if (w == 0) glds_x1(p.labels + (size_t)split * TILE_ROWS + lane, lds_base + LBL_OFF);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  bar();
+  if (grp == 1) bar();
+
+  f32x4 acc[4][2];
+  half8 a[4];
+  for (int it = 0; it < my_tiles; ++it) {
+    const int X = it & 1;
+    const int tile = split + it * tstep;
+    const bool has_next = it + 1 < my_tiles;
+    const int ntile = tile + tstep;
+    if constexpr (MODE == 0) {
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb)
+        theta_next[qb] = __hip_atomic_load(theta_q + 16 * qb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    const int lab = ((const int*)(smem + LBL_OFF + X * TILE_ROWS * 4))[lane];
+    const bool lab_ok = (p.label_filter == MRAG_LABEL_ANY) ? (lab >= 0) : (lab == p.label_filter);
+    const uint64_t tile_mask = __ballot(lab_ok);
+    const char* tb = smem + X * TILE_BYTES;
+    auto read_a = [&](int kk, int rb) {
+      a[rb] = *(const half8*)(tb + ((offA0 ^ ((kk & 3) << 6)) + (kk >> 2) * 256 + rb * 16 * ROW_BYTES));
+    };
+#pragma unroll
+    for (int rb = 0; rb < 4; ++rb) read_a(0, rb);
+    auto kstep = [&](auto kk_c, bool issue) {
+      constexpr int kk = decltype(kk_c)::value;
+      constexpr int pc0 = (kk % HALF) * PPK;  // first piece issued in this k-step of the issue phase
+#pragma unroll
+      for (int rb = 0; rb < 4; ++rb) {
+        if constexpr (kk == 0) {
+          mfma16_ab0(acc[rb][0], a[rb], qf[kk][0]);
+          mfma16_ab0(acc[rb][1], a[rb], qf[kk][1]);
+        } else {
+          mfma16_ab(acc[rb][0], a[rb], qf[kk][0]);
+          mfma16_ab(acc[rb][1], a[rb], qf[kk][1]);
+        }
+        if constexpr (kk + 1 < KSTEPS) read_a(kk + 1, rb);
+        if (rb < PPK && pc0 + rb < PIECES && issue) stage_piece(X ^ 1, ntile, pc0 + rb);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    };
+    // phase 0: group B issues its pieces of the next tile
+    static_for<HALF>([&](auto kk_c) { kstep(kk_c, grp == 1 && has_next); });
+    if (grp == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    bar();
+    // phase 1: group A issues its pieces (and the labels) of the next tile
+    if (grp == 0 && w == 0 && has_next)
+      glds_x1(p.labels + (size_t)ntile * TILE_ROWS + lane, lds_base + LBL_OFF + (X ^ 1) * TILE_ROWS * 4);
+    static_for<HALF>([&](auto kk_c) {
+      kstep(std::integral_constant<int, decltype(kk_c)::value + HALF>{}, grp == 0 && has_next);
+    });
+    mfma16_guard8(acc);
+    if (tile_mask != ~0ull) {
+      const uint64_t lm = tile_mask >> (4 * g4);
+#pragma unroll
+      for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const bool ok = (lm >> (16 * rb + r)) & 1ull;
+          acc[rb][0][r] = ok ? acc[rb][0][r] : -INFINITY;
+          acc[rb][1][r] = ok ? acc[rb][1][r] : -INFINITY;
+        }
+    }
+    const int prow = tile * TILE_ROWS + 4 * g4;
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+      for (int rb = 0; rb < 4; ++rb) {
+        const f32x4& av = acc[rb][qb];
+        const float gm = fmaxf(fmaxf(av[0], av[1]), fmaxf(av[2], av[3]));
+        if constexpr (MODE == 1) {
+          smax[qb] = fmaxf(smax[qb], gm);
+        } else {
+          if (__any(gm > fmaxf(ls[qb][KL3 - 1], theta_f[qb]))) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float sv = av[r];
+              if (sv > fmaxf(ls[qb][KL3 - 1], theta_f[qb])) list_insert<KL3>(ls[qb], li[qb], sv, prow + 16 * rb + r);
+            }
+            if (may_publish && li[qb][KL3 - 1] >= 0 && ls[qb][KL3 - 1] > published[qb]) {
+              published[qb] = ls[qb][KL3 - 1];
+              __hip_atomic_fetch_max(theta_q + 16 * qb, mrag_f2ord(published[qb]), __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT);
+            }
+          }
+        }
+      }
+    if constexpr (MODE == 0) {
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb)
+        if (theta_next[qb] != 0) theta_f[qb] = fmaxf(theta_f[qb], mrag_ord2f(theta_next[qb]));
+    }
+    if (grp == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    bar();
+  }
+  if (grp == 0) bar();  // same barrier count for both groups
+
+  if constexpr (MODE == 1) {
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) {
+      const float m = fmaxf(smax[qb], __shfl_xor(smax[qb], 16));
+      if ((g4 & 1) == 0) p.part_s[((size_t)split * p.Qp + slot0 + 16 * qb) * 2 + (g4 >> 1)] = m;
+    }
+    return;
+  }
+  // fold the four lanes of each query (lanes c16 + 16 g) into one 8-list on g4 == 0 (as v3)
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    float fs[8];
+    int fi[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      fs[j] = j < KL3 ? ls[qb][j] : -INFINITY;
+      fi[j] = j < KL3 ? li[qb][j] : -1;
+    }
+    float tau = li[qb][KL3 - 1] >= 0 ? ls[qb][KL3 - 1] : -INFINITY;
+#pragma unroll
+    for (int o = 16; o < 64; o += 16) {
+#pragma unroll
+      for (int j = 0; j < KL3; ++j) {
+        const float ps = __shfl_xor(ls[qb][j], o);
+        const int pi = __shfl_xor(li[qb][j], o);
+        if (pi >= 0 && ps > fs[7]) list_insert<8>(fs, fi, ps, pi);
+      }
+      const int plast = __shfl_xor(li[qb][KL3 - 1], o);
+      const float pl = __shfl_xor(ls[qb][KL3 - 1], o);
+      if (plast >= 0) tau = fmaxf(tau, pl);
+    }
+    if (g4 == 0) {
+      const int slot = slot0 + 16 * qb;
+      float* os = p.part_s + ((size_t)split * p.Qp + slot) * 8;
+      int32_t* oi = p.part_i + ((size_t)split * p.Qp + slot) * 8;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        os[j] = fs[j];
+        oi[j] = fi[j];
+      }
+      if (fi[7] >= 0) tau = fmaxf(tau, fs[7]);
+      p.part_tau[(size_t)split * p.Qp + slot] = tau;
+    }
+  }
+}
+
 // Seed of the shared threshold from the sample pre-pass: per query, the k-th largest of the
 // 2*splits sample maxima (maxima of disjoint row sets, so k distinct rows score at least
 // that), lowered by a margin of 2.5 EPS so that a seed equal to the k-th best approximate
@@ -1564,6 +1825,24 @@ scan_fn get_scan3(int DP, bool sample = false) {
   }
 }
 
+scan_fn get_scan4(int DP, bool sample = false) {
+  switch (DP) {
+    case 128: return sample ? knn_scan4_kernel<128, 1> : knn_scan4_kernel<128>;
+    case 256: return sample ? knn_scan4_kernel<256, 1> : knn_scan4_kernel<256>;
+    case 384: return sample ? knn_scan4_kernel<384, 1> : knn_scan4_kernel<384>;
+    case 512: {
+      static const int ppk = [] {  // env MRAG_SCAN4_PPK=1/2/4: DMA pieces per k-step (A/B timing)
+        const char* e = getenv("MRAG_SCAN4_PPK");
+        return e ? atoi(e) : 4;
+      }();
+      if (ppk == 1) return sample ? knn_scan4_kernel<512, 1, 1> : knn_scan4_kernel<512, 0, 1>;
+      if (ppk == 2) return sample ? knn_scan4_kernel<512, 1, 2> : knn_scan4_kernel<512, 0, 2>;
+      return sample ? knn_scan4_kernel<512, 1> : knn_scan4_kernel<512>;
+    }
+    default: return nullptr;
+  }
+}
+
 scan_fn get_scan(int DP, int KL, bool collect) {
   switch (DP) {
     case 128: return pick_scan<128>(KL, collect);
@@ -1596,6 +1875,7 @@ struct mrag_knn_index {
   bool scan_v1 = false;  // env MRAG_SCAN_V1=1: force the v1 top-k scan (A/B timing)
   bool no_sample = false;  // env MRAG_SCAN_NO_SAMPLE=1: skip the threshold pre-pass (A/B timing)
   bool scan_v2 = false;    // env MRAG_SCAN_V2=1: the 32x32x16 v2 scan instead of v3 (A/B timing)
+  bool scan_v4 = false;    // env MRAG_SCAN_V4=1: the two-waves-per-SIMD v4 scan instead of v3 (A/B timing)
   int32_t* host_counters = nullptr;  // pinned [2]: fail_cnt, overflow
   mrag_knn::Workspace gws[8];  // K7g buffers
   int64_t last_uncertified = 0, last_retries = 0;
@@ -1664,6 +1944,7 @@ int mrag_knn_create(int32_t dim, int32_t device, mrag_knn_index** out) {
   if (const char* v1 = getenv("MRAG_SCAN_V1")) ix->scan_v1 = atoi(v1) != 0;
   if (const char* ns = getenv("MRAG_SCAN_NO_SAMPLE")) ix->no_sample = atoi(ns) != 0;
   if (const char* v2 = getenv("MRAG_SCAN_V2")) ix->scan_v2 = atoi(v2) != 0;
+  if (const char* v4 = getenv("MRAG_SCAN_V4")) ix->scan_v4 = atoi(v4) != 0;
   hipError_t e = hipStreamCreateWithFlags(&ix->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipHostMalloc((void**)&ix->host_counters, 16, hipHostMallocDefault);
   if (e != hipSuccess) {
@@ -1921,7 +2202,8 @@ int mrag_knn_search(mrag_knn_index* ix, const float* queries, int64_t nq, int32_
     sp.k = k;
     sp.part_tau = use_v3 ? (float*)ix->part_tau.p : nullptr;
 
-    scan_fn scan = use_v3 ? get_scan3(DP) : use_v2 ? get_scan2(DP) : get_scan(DP, KL, false);
+    const bool use_v4 = use_v3 && ix->scan_v4;
+    scan_fn scan = use_v4 ? get_scan4(DP) : use_v3 ? get_scan3(DP) : use_v2 ? get_scan2(DP) : get_scan(DP, KL, false);
     if (DP == 512 && use_v3 && ix->ablate > 20) {  // timing only
       switch (ix->ablate) {
         case 21: scan = knn_scan3_kernel<512, 1>; break;
@@ -1952,14 +2234,17 @@ int mrag_knn_search(mrag_knn_index* ix, const float* queries, int64_t nq, int32_
     if (use_v2 && !ix->no_sample && min_tiles >= 4 * sample_stride) {
       sp.sample_stride = sample_stride;
       sp.sample_tiles = min_tiles / sample_stride;
-      hipLaunchKernelGGL(use_v3 ? get_scan3(DP, true) : get_scan2(DP, true), sgrid, dim3(SCAN2_THREADS), 0, s, sp);
+      if (use_v4)
+        hipLaunchKernelGGL(get_scan4(DP, true), sgrid, dim3(SCAN4_THREADS), 0, s, sp);
+      else
+        hipLaunchKernelGGL(use_v3 ? get_scan3(DP, true) : get_scan2(DP, true), sgrid, dim3(SCAN2_THREADS), 0, s, sp);
       MRAG_CHECK_LAUNCH();
       hipLaunchKernelGGL(theta_init_kernel, dim3((unsigned)nq), dim3(64), 0, s, (const float*)sp.part_s, 2 * S,
                          (int)Qp, k, sp.theta);
       MRAG_CHECK_LAUNCH();
     }
     if (ix->profile) MRAG_HIP(hipEventRecord(ix->ev0, s));
-    hipLaunchKernelGGL(scan, sgrid, dim3(use_v2 ? SCAN2_THREADS : SCAN_THREADS), 0, s, sp);
+    hipLaunchKernelGGL(scan, sgrid, dim3(use_v4 ? SCAN4_THREADS : use_v2 ? SCAN2_THREADS : SCAN_THREADS), 0, s, sp);
     MRAG_CHECK_LAUNCH();
     if (ix->profile) MRAG_HIP(hipEventRecord(ix->ev1, s));
 
