@@ -1033,6 +1033,359 @@ __global__ __launch_bounds__(SCAN2_THREADS) void knn_scan3_kernel(ScanParams p) 
 }
 
 // ---------------------------------------------------------------------------
+// K7 v5 = v3 with three LDS tile buffers of 48 rows (3 x 48 KiB at DP = 512) instead of two of 64:
+// the LDS-DMA of tile t + 2 is issued in the first k-steps of tile t and stays in flight across
+// the end-of-tile barrier (counted vmcnt, raw s_barrier), so a tile's pieces have two tile
+// durations to land instead of most of one — the v3 ablations put 0.12-0.15 ms of its 0.85-0.9 ms
+// on waiting for that DMA. Lists, group tests, part_tau, threshold publishing and outputs are
+// exactly v3's; 3 row blocks of 16 per tile (12 MFMA 16x16x32 per k-step, 12 group tests per
+// tile). The index capacity is a multiple of 768 rows so 48-row tiles never leave it.
+constexpr int T5_ROWS = 48;
+constexpr int T5_RB = T5_ROWS / 16;
+constexpr int T5_NBUF = 3;
+
+__device__ __forceinline__ void mfma16_guard3(f32x4 (&acc)[T5_RB][4]) {
+  asm volatile("s_nop 15\n\ts_nop 3"
+               : "+v"(acc[0][0]), "+v"(acc[0][1]), "+v"(acc[0][2]), "+v"(acc[0][3]), "+v"(acc[1][0]),
+                 "+v"(acc[1][1]), "+v"(acc[1][2]), "+v"(acc[1][3]), "+v"(acc[2][0]), "+v"(acc[2][1]),
+                 "+v"(acc[2][2]), "+v"(acc[2][3]));
+}
+
+template <int DP, int ABL = 0, int MODE = 0, int FRONT = 3>
+__global__ __launch_bounds__(SCAN2_THREADS) void knn_scan5_kernel(ScanParams p) {
+  constexpr int KSTEPS = DP / 32;
+  constexpr int ROW_BYTES = DP * 2;
+  constexpr int TILE_BYTES = T5_ROWS * ROW_BYTES;
+  constexpr int CPR = DP / 8;
+  // a 48-row tile is 12 / 24 / 36 / 48 pieces of 1 KB (one LDS-DMA instruction each) at DP =
+  // 128 / 256 / 384 / 512: when the waves do not divide them, wave w takes pieces w, w + W, ...
+  // (GLDS_PER_WAVE or GLDS_PER_WAVE - 1 of them), otherwise a contiguous run
+  constexpr int NPIECES = TILE_BYTES / 1024;
+  constexpr bool EVEN = NPIECES % SCAN2_WAVES == 0;
+  constexpr int GLDS_PER_WAVE = (NPIECES + SCAN2_WAVES - 1) / SCAN2_WAVES;
+  static_assert(TILE_BYTES % 1024 == 0, "whole pieces");
+  static_assert(GLDS_PER_WAVE <= FRONT * KSTEPS && FRONT <= T5_RB, "the next-next tile's pieces fit the k-steps");
+  static_assert(CPR % 16 == 0, "swizzle needs rows of a multiple of 16 chunks");
+  static_assert(CPR != 64 || EVEN, "the DP = 512 DMA path assumes contiguous pieces");
+  constexpr bool NO_EPI = ABL == 1 || ABL == 4;
+  constexpr bool NO_GLDS = ABL == 4;
+  constexpr int NGROUPS = 4 * T5_RB;  // group g: query block g / T5_RB, row block g % T5_RB
+  constexpr int LBL_OFF = T5_NBUF * TILE_BYTES;
+  // shared thresholds of the workgroup's query slots, one copy per tile parity: wave w DMAs its
+  // 64 slots (lane = 16 qb + c16) into THETA_OFF + X * THETA_SET + 256 w
+  constexpr int THETA_OFF = LBL_OFF + T5_NBUF * 256;
+  constexpr int THETA_SET = SCAN2_WAVES * 256;
+  static_assert(QPW2 == 64, "one 64-slot theta row per wave");
+  constexpr uint64_t FULL = (1ull << T5_ROWS) - 1;
+  __shared__ __attribute__((aligned(16))) char smem[THETA_OFF + 2 * THETA_SET];
+
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g4 = lane >> 4;
+  const int c16 = lane & 15;
+  const uint32_t lds_base = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)((AS3 char*)smem));
+
+  int qg, split;  // same XCD-aware block mapping as v1 / v2
+  {
+    const int b = blockIdx.x;
+    if ((p.splits & 7) == 0) {
+      const int xcd = b & 7, sl = b >> 3;
+      qg = sl % p.qgroups;
+      split = (sl / p.qgroups) * 8 + xcd;
+    } else {
+      qg = b % p.qgroups;
+      split = b / p.qgroups;
+    }
+  }
+  // query slot of block qb is slot0 + 16 qb; Qp is a multiple of QPG so every slot exists
+  const int slot0 = qg * QPG + w * QPW2 + c16;
+
+  half8 qf[KSTEPS][4];
+#pragma unroll
+  for (int kk = 0; kk < KSTEPS; ++kk)
+#pragma unroll
+    for (int qb = 0; qb < 4; ++qb)
+      qf[kk][qb] = *(const half8*)(p.q16 + (size_t)(slot0 + 16 * qb) * DP + kk * 32 + g4 * 8);
+#pragma unroll
+  for (int kk = 0; kk < KSTEPS; ++kk)
+    asm volatile("" ::"a"(qf[kk][0]), "a"(qf[kk][1]), "a"(qf[kk][2]), "a"(qf[kk][3]));
+
+  float ls[4][KL3];
+  int li[4][KL3];
+#pragma unroll
+  for (int qb = 0; qb < 4; ++qb)
+#pragma unroll
+    for (int j = 0; j < KL3; ++j) {
+      ls[qb][j] = -INFINITY;
+      li[qb][j] = -1;
+    }
+  float theta_f[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+  uint32_t theta_next[4] = {0u, 0u, 0u, 0u};
+  float published[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+  uint32_t* const theta_q = p.theta + slot0;
+  const bool may_publish = p.k <= KL3;
+
+  // A fragment of row 16 rb + c16, chunk 4 kk + g4, sits at chunk (4 kk + g4) ^ c16: byte
+  // offset (offA0 ^ ((kk & 3) << 6)) + (kk >> 2) * 256 + rb * 16 * ROW_BYTES
+  const int offA0_init = c16 * ROW_BYTES + 16 * (g4 ^ c16);
+
+  f32x4 acc[2][T5_RB][4];  // [buffer][row block][query block]
+#pragma unroll
+  for (int i = 0; i < T5_RB; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      acc[1][i][j] = f32x4{-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+      acc[0][i][j] = f32x4{};
+    }
+
+  int my_tiles = (split < p.ntiles) ? (p.ntiles - 1 - split) / p.splits + 1 : 0;
+  int tstep = p.splits;
+  if constexpr (MODE == 1) {
+    my_tiles = min(my_tiles, p.sample_tiles);
+    tstep = p.splits * p.sample_stride;
+  }
+  float smax[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+
+  const int my_pieces = EVEN ? GLDS_PER_WAVE : (NPIECES - w + SCAN2_WAVES - 1) / SCAN2_WAVES;  // wave-uniform
+  auto stage_piece = [&](int buf, int tile, int i, int lane_t) {
+    const char* gt = (const char*)p.x16 + (size_t)tile * TILE_BYTES;
+    const unsigned piece = EVEN ? w * GLDS_PER_WAVE + i : i * SCAN2_WAVES + w;
+    const unsigned P = piece * 64 + (unsigned)lane_t;
+    const unsigned row = P / CPR;
+    const unsigned pos = P - row * CPR;
+    const unsigned c = pos ^ (row & 15);
+    glds_x4(gt + row * ROW_BYTES + c * 16, lds_base + buf * TILE_BYTES + piece * 1024);
+  };
+  auto stage_labels = [&](int buf, int tile) {  // lanes >= T5_ROWS would read the next tile's labels: off
+    if (w == 0 && lane < T5_ROWS) glds_x1(p.labels + (size_t)tile * T5_ROWS + lane, lds_base + LBL_OFF + buf * 256);
+  };
+
+  int prow = 0;  // first row of the filtered tile + 4 g4
+  auto epi_group = [&](auto g_c, auto y_c) {
+    constexpr int G = decltype(g_c)::value;
+    constexpr int Y = decltype(y_c)::value;
+    constexpr int qb = G / T5_RB, rb = G % T5_RB;
+    f32x4& av = acc[Y][rb][qb];
+    if constexpr (NO_EPI) {
+      asm volatile("" ::"v"(av));
+    } else {
+      const float gm = fmaxf(fmaxf(av[0], av[1]), fmaxf(av[2], av[3]));
+      if constexpr (MODE == 1) {
+        smax[qb] = fmaxf(smax[qb], gm);
+        asm volatile("" : "+v"(smax[qb]));
+      } else {
+        if (__any(gm > fmaxf(ls[qb][KL3 - 1], theta_f[qb]))) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float sv = av[r];
+            if (sv > fmaxf(ls[qb][KL3 - 1], theta_f[qb]))
+              list_insert<KL3>(ls[qb], li[qb], sv, prow + 16 * rb + r);
+          }
+          if (may_publish && li[qb][KL3 - 1] >= 0 && ls[qb][KL3 - 1] > published[qb]) {
+            published[qb] = ls[qb][KL3 - 1];
+            __hip_atomic_fetch_max(theta_q + 16 * qb, mrag_f2ord(published[qb]), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+          }
+        }
+      }
+    }
+  };
+
+  // accumulator buffer X = it & 1 (compile time), LDS tile buffer it % 3; the DMA of tile it + 2
+  // goes into buffer (it + 2) % 3, which held tile it - 1 (every wave is past it: barrier)
+  auto tile_body = [&](auto x_c, int it) {
+    constexpr int X = decltype(x_c)::value;
+    constexpr int Y = 1 - X;
+    const int tile = split + it * tstep;
+    const bool has_nn = it + 2 < my_tiles;  // wave-uniform
+    const int ntile = tile + 2 * tstep;
+    const int bi = it % T5_NBUF, bn = (it + 2) % T5_NBUF;
+    const char* gw = (const char*)p.x16 + (size_t)ntile * TILE_BYTES + (size_t)w * GLDS_PER_WAVE * ROW_BYTES;
+    uint32_t ldsw = lds_base + bn * TILE_BYTES + w * GLDS_PER_WAVE * 1024;
+    asm volatile("" : "+s"(gw), "+s"(ldsw));
+    if constexpr (MODE == 0) {
+      // the thresholds travel by LDS-DMA, not into registers: a register loaded by inline asm is
+      // "ready" to the compiler at once, and it may copy it (before the wait) into the register
+      // the consumer wants — that read a stale threshold of another query block. The DMA is older
+      // than this tile's pieces, so the end-of-tile vmcnt(N) retires it (no drain of the ring);
+      // a stale value is a threshold that once held, hence still a valid lower bound
+      glds_x1(theta_q - c16 + lane, lds_base + THETA_OFF + X * THETA_SET + w * 256);
+    }
+    const int lab = ((const int*)(smem + LBL_OFF + bi * 256))[lane];
+    const bool lab_ok = lane < T5_ROWS && ((p.label_filter == MRAG_LABEL_ANY) ? (lab >= 0) : (lab == p.label_filter));
+    const uint64_t tile_mask = __ballot(lab_ok);
+    const char* tb = smem + bi * TILE_BYTES;
+    int lane_t = lane, offA0 = offA0_init;
+    uint32_t lane16 = lane * 16;
+    asm volatile("" : "+v"(lane_t), "+v"(offA0), "+v"(lane16));
+    // DP = 512: m0 holds the piece's LDS address from gap 1 to the DMA in gap 2 (nothing the
+    // compiler emits in this loop reads m0: ds_read_b128 / MFMA / VALU / SALU only); it is saved
+    // once per tile and restored before the barrier
+    uint32_t m0_keep = 0;
+    uint32_t voff = 0;
+    if constexpr (CPR == 64 && !NO_GLDS) asm volatile("s_mov_b32 %0, m0" : "=s"(m0_keep));
+    half8 a[T5_RB];
+    const uint32_t rw = (uint32_t)(GLDS_PER_WAVE * w);  // first tile row of this wave's pieces (DP = 512)
+    auto read_a = [&](int kk, int rb) {
+      a[rb] = *(const half8*)(tb + ((offA0 ^ ((kk & 3) << 6)) + (kk >> 2) * 256 + rb * 16 * ROW_BYTES));
+    };
+#pragma unroll
+    for (int rb = 0; rb < T5_RB; ++rb) read_a(0, rb);
+    if (has_nn) stage_labels(bn, ntile);
+    static_for<KSTEPS>([&](auto kk_c) {
+      constexpr int kk = decltype(kk_c)::value;
+      constexpr int g0 = (kk * NGROUPS + KSTEPS - 1) / KSTEPS;        // this k-step's groups:
+      constexpr int g1 = ((kk + 1) * NGROUPS + KSTEPS - 1) / KSTEPS;  // [g0, g1), at most 4
+      static_for<4 * T5_RB>([&](auto j_c) {
+        constexpr int j = decltype(j_c)::value;
+        constexpr int rb = j >> 2, qb = j & 3;
+        if constexpr (kk == 0)
+          mfma16_ab0(acc[X][rb][qb], a[rb], qf[kk][qb]);
+        else
+          mfma16_ab(acc[X][rb][qb], a[rb], qf[kk][qb]);
+        // one job per MFMA gap
+        if constexpr ((j & 3) == 3) {  // after the last MFMA of block rb: its next fragment
+          if constexpr (kk + 1 < KSTEPS) read_a(kk + 1, rb);
+        } else if constexpr ((j & 3) == 1) {  // piece FRONT kk + (j >> 2): m0 + source offset
+          constexpr int pc = FRONT * kk + (j >> 2);
+          if constexpr (CPR == 64 && !NO_GLDS && (j >> 2) < FRONT && pc < GLDS_PER_WAVE) {
+            voff = (lane16 ^ (((rw + pc) & 15u) << 4)) + (uint32_t)(pc * 1024);
+            asm volatile("s_mov_b32 m0, %1" : "+v"(voff) : "s"(ldsw + pc * 1024));
+          }
+        } else if constexpr ((j & 3) == 2) {  // ... and its DMA
+          constexpr int pc = FRONT * kk + (j >> 2);
+          if constexpr (!NO_GLDS && (j >> 2) < FRONT && pc < GLDS_PER_WAVE) {
+            if (has_nn) {
+              if constexpr (CPR == 64)
+                asm volatile("global_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(gw) : "memory");
+              else if (EVEN || pc < my_pieces)
+                stage_piece(bn, ntile, pc, lane_t);
+            }
+          }
+        } else if constexpr ((j & 3) == 0) {
+          if constexpr (g0 + (j >> 2) < g1)
+            epi_group(std::integral_constant<int, g0 + (j >> 2)>{}, std::integral_constant<int, Y>{});
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      });
+    });
+    mfma16_guard3(acc[X]);
+    if constexpr (CPR == 64 && !NO_GLDS) asm volatile("s_mov_b32 m0, %0" ::"s"(m0_keep));
+    if (tile_mask != FULL) {
+      const uint64_t lm = tile_mask >> (4 * g4);
+#pragma unroll
+      for (int rb = 0; rb < T5_RB; ++rb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const bool ok = (lm >> (16 * rb + r)) & 1ull;
+#pragma unroll
+          for (int qb = 0; qb < 4; ++qb) acc[X][rb][qb][r] = ok ? acc[X][rb][qb][r] : -INFINITY;
+        }
+    }
+    prow = tile * T5_ROWS + 4 * g4;
+    // tile it + 1 (DMA issued during tile it - 1) must have landed; tile it + 2's pieces (the
+    // youngest GLDS_PER_WAVE operations of this wave) stay in flight across the barrier
+    if (has_nn && (EVEN || my_pieces == GLDS_PER_WAVE)) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GLDS_PER_WAVE) : "memory");
+    } else if (!EVEN && has_nn) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(EVEN ? GLDS_PER_WAVE : GLDS_PER_WAVE - 1) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    if constexpr (MODE == 0) {
+      // this wave's own DMA, retired by its vmcnt: no barrier needed; slot X is rewritten two
+      // tiles later, after the lgkmcnt(0) below has returned this read
+      const uint32_t* th = (const uint32_t*)(smem + THETA_OFF + X * THETA_SET + w * 256);
+#pragma unroll
+      for (int qb = 0; qb < 4; ++qb) theta_next[qb] = th[16 * qb + c16];
+#pragma unroll
+      for (int qb = 0; qb < 4; ++qb)
+        if (theta_next[qb] != 0) theta_f[qb] = fmaxf(theta_f[qb], mrag_ord2f(theta_next[qb]));
+      asm volatile("" : "+v"(theta_f[0]), "+v"(theta_f[1]), "+v"(theta_f[2]), "+v"(theta_f[3]));
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    // the barrier intrinsic is not a memory operation to LLVM: without this compiler fence the
+    // next tile's LDS reads (labels, A fragments) may be hoisted above it (MODE 1 has no other
+    // memory-clobbering statement in between) and read a buffer before its DMA has landed
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  if (my_tiles > 0) {
+    // prologue: tiles 0 and 1 into buffers 0 and 1, landed before the first read
+#pragma unroll
+    for (int i = 0; i < GLDS_PER_WAVE; ++i)
+      if (i < my_pieces) stage_piece(0, split, i, lane);
+    stage_labels(0, split);
+    if (my_tiles > 1) {
+#pragma unroll
+      for (int i = 0; i < GLDS_PER_WAVE; ++i)
+        if (i < my_pieces) stage_piece(1, split + tstep, i, lane);
+      stage_labels(1, split + tstep);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int it = 0; it < my_tiles; it += 2) {
+      tile_body(std::integral_constant<int, 0>{}, it);
+      if (it + 1 < my_tiles) tile_body(std::integral_constant<int, 1>{}, it + 1);
+    }
+    if (my_tiles & 1) {
+      static_for<NGROUPS>([&](auto g_c) { epi_group(g_c, std::integral_constant<int, 0>{}); });
+    } else {
+      static_for<NGROUPS>([&](auto g_c) { epi_group(g_c, std::integral_constant<int, 1>{}); });
+    }
+  }
+
+  if constexpr (MODE == 1) {
+    // two maxima per (split, query) over disjoint rows: lane groups {0, 1} and {2, 3}
+#pragma unroll
+    for (int qb = 0; qb < 4; ++qb) {
+      const float m = fmaxf(smax[qb], __shfl_xor(smax[qb], 16));
+      if ((g4 & 1) == 0) p.part_s[((size_t)split * p.Qp + slot0 + 16 * qb) * 2 + (g4 >> 1)] = m;
+    }
+    return;
+  }
+  // fold the four lanes of each query (lanes c16 + 16 g) into one 8-list on g4 == 0
+#pragma unroll
+  for (int qb = 0; qb < 4; ++qb) {
+    float fs[8];
+    int fi[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      fs[j] = j < KL3 ? ls[qb][j] : -INFINITY;
+      fi[j] = j < KL3 ? li[qb][j] : -1;
+    }
+    float tau = li[qb][KL3 - 1] >= 0 ? ls[qb][KL3 - 1] : -INFINITY;
+#pragma unroll
+    for (int o = 16; o < 64; o += 16) {
+#pragma unroll
+      for (int j = 0; j < KL3; ++j) {
+        const float ps = __shfl_xor(ls[qb][j], o);
+        const int pi = __shfl_xor(li[qb][j], o);
+        if (pi >= 0 && ps > fs[7]) list_insert<8>(fs, fi, ps, pi);
+      }
+      const int plast = __shfl_xor(li[qb][KL3 - 1], o);
+      const float pl = __shfl_xor(ls[qb][KL3 - 1], o);
+      if (plast >= 0) tau = fmaxf(tau, pl);
+    }
+    if (g4 == 0) {
+      const int slot = slot0 + 16 * qb;
+      float* os = p.part_s + ((size_t)split * p.Qp + slot) * 8;
+      int32_t* oi = p.part_i + ((size_t)split * p.Qp + slot) * 8;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        os[j] = fs[j];
+        oi[j] = fi[j];
+      }
+      if (fi[7] >= 0) tau = fmaxf(tau, fs[7]);
+      p.part_tau[(size_t)split * p.Qp + slot] = tau;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // K7 v4 (top-k mode and sample pre-pass; same lists, part_tau and outputs as v3): two waves per
 // SIMD instead of one, so one wave's MFMAs cover its sibling's LDS-DMA issue, end-of-tile
 // waits, barriers and filter work.
@@ -1142,6 +1495,7 @@ __global__ __launch_bounds__(SCAN4_THREADS) void knn_scan4_kernel(ScanParams p) 
   auto bar = [&]() {
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");  // compiler fence: LDS reads stay after the barrier
     __builtin_amdgcn_sched_barrier(0);
   };
 
@@ -1187,7 +1541,16 @@ __global__ __launch_bounds__(SCAN4_THREADS) void knn_scan4_kernel(ScanParams p) 
           mfma16_ab(acc[rb][1], a[rb], qf[kk][1]);
         }
         if constexpr (kk + 1 < KSTEPS) read_a(kk + 1, rb);
-        if (rb < PPK && pc0 + rb < PIECES && issue) stage_piece(X ^ 1, ntile, pc0 + rb);
+        if (rb < PPK && pc0 + rb < PIECES && issue) {
+          if constexpr (CPR == 64) {  // DP = 512: a piece is one row; SGPR row base + one VALU offset
+            const int pc = pc0 + rb, row = 8 * w + pc;
+            const char* gw = (const char*)p.x16 + (size_t)ntile * TILE_BYTES + (size_t)(8 * w) * ROW_BYTES;
+            const uint32_t voff = ((uint32_t)lane ^ (uint32_t)(row & 15)) * 16u + (uint32_t)(pc * 1024);
+            glds_x4_saddr(voff, gw, lds_base + (uint32_t)((X ^ 1) * TILE_BYTES + row * 1024));
+          } else {
+            stage_piece(X ^ 1, ntile, pc0 + rb);
+          }
+        }
         __builtin_amdgcn_sched_barrier(0);
       }
     };
@@ -1825,6 +2188,16 @@ scan_fn get_scan3(int DP, bool sample = false) {
   }
 }
 
+scan_fn get_scan5(int DP, bool sample = false) {
+  switch (DP) {
+    case 128: return sample ? knn_scan5_kernel<128, 0, 1> : knn_scan5_kernel<128>;
+    case 256: return sample ? knn_scan5_kernel<256, 0, 1> : knn_scan5_kernel<256>;
+    case 384: return sample ? knn_scan5_kernel<384, 0, 1> : knn_scan5_kernel<384>;
+    case 512: return sample ? knn_scan5_kernel<512, 0, 1> : knn_scan5_kernel<512>;
+    default: return nullptr;
+  }
+}
+
 scan_fn get_scan4(int DP, bool sample = false) {
   switch (DP) {
     case 128: return sample ? knn_scan4_kernel<128, 1> : knn_scan4_kernel<128>;
@@ -1876,6 +2249,7 @@ struct mrag_knn_index {
   bool no_sample = false;  // env MRAG_SCAN_NO_SAMPLE=1: skip the threshold pre-pass (A/B timing)
   bool scan_v2 = false;    // env MRAG_SCAN_V2=1: the 32x32x16 v2 scan instead of v3 (A/B timing)
   bool scan_v4 = false;    // env MRAG_SCAN_V4=1: the two-waves-per-SIMD v4 scan instead of v3 (A/B timing)
+  bool scan_v5 = false;    // env MRAG_SCAN_V5=1: the three-buffer 48-row v5 scan instead of v3
   int32_t* host_counters = nullptr;  // pinned [2]: fail_cnt, overflow
   mrag_knn::Workspace gws[8];  // K7g buffers
   int64_t last_uncertified = 0, last_retries = 0;
@@ -1891,7 +2265,7 @@ namespace {
 int grow(mrag_knn_index* ix, int64_t need) {
   if (need <= ix->cap) return MRAG_OK;
   int64_t ncap = std::max<int64_t>({(int64_t)TILE_ROWS, ix->cap * 2, need});
-  ncap = (ncap + 255) / 256 * 256;  // a multiple of the 64-row scan tile and of K7g's 128-column GEMM tile
+  ncap = (ncap + 767) / 768 * 768;  // a multiple of the 64- and 48-row scan tiles and of K7g's 128-column GEMM tile
   DevBuf nx16, nx32, nxn, nlab;
   if (int rc = ensure(nx16, (size_t)ncap * ix->DP * 2)) return rc;
   if (int rc = ensure(nx32, (size_t)ncap * ix->DP * 4)) return rc;
@@ -1945,6 +2319,7 @@ int mrag_knn_create(int32_t dim, int32_t device, mrag_knn_index** out) {
   if (const char* ns = getenv("MRAG_SCAN_NO_SAMPLE")) ix->no_sample = atoi(ns) != 0;
   if (const char* v2 = getenv("MRAG_SCAN_V2")) ix->scan_v2 = atoi(v2) != 0;
   if (const char* v4 = getenv("MRAG_SCAN_V4")) ix->scan_v4 = atoi(v4) != 0;
+  if (const char* v5 = getenv("MRAG_SCAN_V5")) ix->scan_v5 = atoi(v5) != 0;
   hipError_t e = hipStreamCreateWithFlags(&ix->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipHostMalloc((void**)&ix->host_counters, 16, hipHostMallocDefault);
   if (e != hipSuccess) {
@@ -2203,7 +2578,15 @@ int mrag_knn_search(mrag_knn_index* ix, const float* queries, int64_t nq, int32_
     sp.part_tau = use_v3 ? (float*)ix->part_tau.p : nullptr;
 
     const bool use_v4 = use_v3 && ix->scan_v4;
-    scan_fn scan = use_v4 ? get_scan4(DP) : use_v3 ? get_scan3(DP) : use_v2 ? get_scan2(DP) : get_scan(DP, KL, false);
+    const bool use_v5 = use_v3 && !use_v4 && ix->scan_v5;
+    // v5 tiles are 48 rows: its scan and pre-pass walk ntiles5 tiles (the collect pass keeps 64)
+    const int ntiles5 = (int)((ix->n + T5_ROWS - 1) / T5_ROWS);
+    if (use_v5) sp.ntiles = ntiles5;
+    scan_fn scan = use_v5   ? get_scan5(DP)
+                   : use_v4 ? get_scan4(DP)
+                   : use_v3 ? get_scan3(DP)
+                   : use_v2 ? get_scan2(DP)
+                            : get_scan(DP, KL, false);
     if (DP == 512 && use_v3 && ix->ablate > 20) {  // timing only
       switch (ix->ablate) {
         case 21: scan = knn_scan3_kernel<512, 1>; break;
@@ -2230,12 +2613,14 @@ int mrag_knn_search(mrag_knn_index* ix, const float* queries, int64_t nq, int32_
       const int v = e ? atoi(e) : 16;
       return v >= 2 ? v : 16;
     }();
-    const int min_tiles = ntiles / S;
+    const int min_tiles = sp.ntiles / S;
     if (use_v2 && !ix->no_sample && min_tiles >= 4 * sample_stride) {
       sp.sample_stride = sample_stride;
       sp.sample_tiles = min_tiles / sample_stride;
       if (use_v4)
         hipLaunchKernelGGL(get_scan4(DP, true), sgrid, dim3(SCAN4_THREADS), 0, s, sp);
+      else if (use_v5)
+        hipLaunchKernelGGL(get_scan5(DP, true), sgrid, dim3(SCAN2_THREADS), 0, s, sp);
       else
         hipLaunchKernelGGL(use_v3 ? get_scan3(DP, true) : get_scan2(DP, true), sgrid, dim3(SCAN2_THREADS), 0, s, sp);
       MRAG_CHECK_LAUNCH();
@@ -2247,6 +2632,7 @@ int mrag_knn_search(mrag_knn_index* ix, const float* queries, int64_t nq, int32_
     hipLaunchKernelGGL(scan, sgrid, dim3(use_v4 ? SCAN4_THREADS : use_v2 ? SCAN2_THREADS : SCAN_THREADS), 0, s, sp);
     MRAG_CHECK_LAUNCH();
     if (ix->profile) MRAG_HIP(hipEventRecord(ix->ev1, s));
+    sp.ntiles = ntiles;  // 64-row tiles for the collect pass
 
     MergeParams mp{};
     mp.part_s = sp.part_s;
