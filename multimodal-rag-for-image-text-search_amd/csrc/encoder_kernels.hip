@@ -569,6 +569,234 @@ __global__ __launch_bounds__(G8_THREADS) void gemm_8p_kernel(GemmArgs g) {
 }
 
 // ---------------------------------------------------------------------------
+// K3e (M >= 1024, N % 256 == 0, K % 64 == 0): persistent, one workgroup per CU, 256 x 256
+// tiles, FOUR waves (2 x 2) of 128 x 128 — one wave per SIMD owning a quarter of the tile, so
+// every fragment a wave reads from LDS feeds 8 MFMAs (K3d's 128 x 64 waves: 4 or 8) and the
+// CU reads 128 KiB of fragments per 64 k instead of 192 KiB.
+//  * accumulators: 8 x 8 blocks of 16 x 16 per wave = 256 f32 per lane, AGPR-resident (asm
+//    MFMA operands);
+//  * LDS: two 64-KiB K-tiles (A: 256 rows x 128 B, then B: 256 rows x 128 B), 16-byte chunk c
+//    of row j at position c ^ ((j >> 1) & 7) (K3's conflict-free image). Rows of 128 B = 64 k
+//    keep every LDS-DMA request a whole 128-byte line (rows of 64 B doubled the L2 requests:
+//    notes/gemm_experiments.md);
+//  * a K-tile is consumed in two 32-deep halves with one fragment set per half (R0, R1: 64
+//    VGPRs each): half 0 of tile t runs on R0 while R1 is read from tile t; half 1 runs on R1
+//    while R0 is read from tile t + 1. Tile t is fully read once half 0 ends, so the single
+//    barrier per K-tile sits there: wait for K-tile t + 1 (own vmcnt), barrier, then the
+//    LDS-DMA of K-tile t + 2 into tile t's buffer is spread over half 1's MFMAs. The load stream
+//    runs across output tiles, so the epilogue overlaps the next tile's loads;
+//  * waves 0, 1 stage the A half of every K-tile, waves 2, 3 the B half: 16 one-KiB pieces (8
+//    rows of 128 B) per wave per K-tile through the SADDR form (lane part of the offset in a
+//    VGPR, the piece's row offset and k in SGPRs);
+//  * C^T blocks with the weight fragment as MFMA operand A and permuted weight rows, so a lane
+//    stores 8 consecutive columns (gemm_store8) — the same per-element accumulation order
+//    (32-deep chunks in ascending k, one accumulator) and epilogue as K3 / K3d, hence the same
+//    bits whichever kernel a batch size selects.
+constexpr int G4_THREADS = 256;
+constexpr int G4_SLOT = 65536;  // one 64-deep K-tile: A 32 KiB + B 32 KiB
+
+__device__ __forceinline__ void glds_x4_saddr(uint32_t voff, const void* sbase, uint32_t lds_addr) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(sbase), "s"(lds_addr)
+      : "memory");
+}
+
+// weight LDS row j (0..127 within a wave column) -> its tile column: lane group f of block pair
+// (2p, 2p + 1) owns the 8 consecutive columns 32 p + 8 f + 0..7. For j = 8 q + rr this splits
+// into a piece part (uniform) and a lane part.
+__device__ __forceinline__ constexpr int g4_colbase(int q) { return 32 * (q >> 2) + 16 * (q & 1) + 4 * ((q >> 1) & 1); }
+__device__ __forceinline__ constexpr int g4_collane(int rr) { return 8 * (rr >> 2) + (rr & 3); }
+
+template <int EPI>
+__global__ __launch_bounds__(G4_THREADS) void gemm_4w_kernel(GemmArgs g) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * G4_SLOT + G8_BIAS_MAX * 4];
+  float* sbias = (float*)(smem + 2 * G4_SLOT);
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = w >> 1, wc = w & 1;
+  const int fr = lane & 15, fq = lane >> 4;
+  const uint32_t lds_base = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)((AS3 char*)smem));
+
+  // tiles: XCD x owns a contiguous range of tile ids (tm-major), round-robin over its workgroups
+  const int tiles_n = g.N / 256;
+  const int ntiles = ((g.M + 255) / 256) * tiles_n;
+  const int xcd = blockIdx.x & 7, sidx = blockIdx.x >> 3;
+  const int nbx = ((int)gridDim.x - xcd + 7) >> 3;
+  const int q8 = ntiles >> 3, r8 = ntiles & 7;
+  const int lo = xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8;
+  const int cnt = q8 + (xcd < r8 ? 1 : 0);
+  const int my_n = sidx < cnt ? (cnt - sidx + nbx - 1) / nbx : 0;
+  if (my_n == 0) return;  // whole workgroup, before any barrier
+
+  for (int i = threadIdx.x; i < g.N; i += G4_THREADS) sbias[i] = g.bias ? g.bias[i] : 0.f;
+
+  const int ktiles = g.K / 64;
+  const int total = my_n * ktiles;
+
+  // loader: piece q (0..15) of this wave = LDS rows 8 (16 (w & 1) + q) + rr, rr = lane >> 3, of
+  // the A half (waves 0, 1) or the B half (waves 2, 3); lane position lane & 7 holds source
+  // chunk (lane & 7) ^ ((row >> 1) & 7) (row & 15 = 8 (q & 1) + rr)
+  const bool loadsB = w >= 2;
+  const int rr = lane >> 3;
+  const uint32_t cb0 = (uint32_t)(((lane & 7) ^ (rr >> 1)) * 16);        // q even
+  const uint32_t cb1 = (uint32_t)(((lane & 7) ^ (4 + (rr >> 1))) * 16);  // q odd
+  const uint32_t ldb = (uint32_t)(loadsB ? g.ldw : g.lda) * 2u;          // row stride, bytes
+  const uint32_t vlaneB = (uint32_t)g4_collane(rr) * ldb;
+  const uint32_t lds_w = lds_base + (loadsB ? 32768u : 0u) + (uint32_t)(w & 1) * 16384u;
+  int ld_kt = 0, ld_T = lo + sidx;
+  int ld_m0 = 0, ld_n0 = 0;
+  auto load_tile_origin = [&]() {
+    const int tm = ld_T / tiles_n;
+    ld_m0 = tm * 256;
+    ld_n0 = (ld_T - tm * tiles_n) * 256;
+  };
+  load_tile_origin();
+  // piece q of K-tile L[t]: A rows ld_m0 + 128 (w & 1) + 8 q + rr (clamped to M - 1), B rows
+  // ld_n0 + 128 (w & 1) + g4_colbase(q) + g4_collane(rr)
+  auto issue_piece = [&](int t, int q) {
+    const uint32_t dst = lds_w + (uint32_t)(t & 1) * G4_SLOT + (uint32_t)q * 1024u;
+    const uint32_t cb = (q & 1) ? cb1 : cb0;
+    if (loadsB) {
+      const char* sb = (const char*)(g.W + (size_t)(ld_n0 + 128 * (w & 1) + g4_colbase(q)) * g.ldw + ld_kt * 64);
+      glds_x4_saddr(vlaneB + cb, sb, dst);
+    } else {
+      // rows past M re-read row M - 1: base row and lane row both clamped, so 0 <= row < M
+      const int rbase = min(ld_m0 + 128 * (w & 1) + 8 * q, g.M - 1);
+      const char* sb = (const char*)(g.A + (size_t)rbase * g.lda + ld_kt * 64);
+      const uint32_t row = (uint32_t)min(rr, g.M - 1 - rbase);
+      glds_x4_saddr(row * ldb + cb, sb, dst);
+    }
+  };
+  auto advance_loader = [&]() {
+    if (++ld_kt == ktiles) {
+      ld_kt = 0;
+      ld_T += nbx;
+      if (ld_T < ntiles) load_tile_origin();
+    }
+  };
+
+  // fragments: activation block i -> LDS A row 128 wr + 16 i + fr, weight block jb -> LDS B row
+  // 128 wc + 16 jb + fr; half kk reads chunk 4 kk + fq; blocks 2 KiB apart
+  int offA[2], offB[2];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+    offA[kk] = swz_off(128 * wr + fr, 4 * kk + fq);
+    offB[kk] = 32768 + swz_off(128 * wc + fr, 4 * kk + fq);
+  }
+  half8 fa[2][8], fb[2][8];  // [half][block]
+
+  f32x4 acc[8][8];  // [activation block i][weight block jb], AGPR-resident (asm MFMA operand)
+  constexpr int SPB = (EPI == EPI_F32_RESIDUAL || EPI == EPI_F32) ? 2 : 1;
+  constexpr int ST_FULL = 32 * SPB;  // vector stores of a full tile's epilogue per wave
+  constexpr int ST_WAIT = ST_FULL < 63 ? ST_FULL : 63;
+  bool post = false;     // an epilogue ran since the last K-tile wait ...
+  bool st_full = true;   // ... and issued ST_FULL stores (else fewer: partial tile)
+
+  auto mfma_row = [&](int kk, int i) {
+#pragma unroll
+    for (int jb = 0; jb < 8; ++jb)
+      asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+a"(acc[i][jb]) : "v"(fb[kk][jb]), "v"(fa[kk][i]));
+  };
+
+  // prologue: K-tiles 0, 1 in flight, K-tile 0 landed; R0 <- K-tile 0 half 0
+#pragma unroll
+  for (int q = 0; q < 16; ++q) issue_piece(0, q);
+  advance_loader();
+  if (total > 1) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) issue_piece(1, q);
+    advance_loader();
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();  // also publishes sbias
+#pragma unroll
+  for (int b = 0; b < 8; ++b) {
+    fa[0][b] = *(const half8*)(smem + offA[0] + b * 2048);
+    fb[0][b] = *(const half8*)(smem + offB[0] + b * 2048);
+  }
+
+  int t = 0;
+  for (int tl = 0; tl < my_n; ++tl) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int jb = 0; jb < 8; ++jb) acc[i][jb] = f32x4{};
+    for (int kt = 0; kt < ktiles; ++kt, ++t) {
+      const char* cur = (const char*)smem + (t & 1) * G4_SLOT;
+      const char* nxt = (const char*)smem + ((t + 1) & 1) * G4_SLOT;
+      // half 0 on R0; R1 <- this K-tile's half 1
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        mfma_row(0, i);
+        fa[1][i] = *(const half8*)(cur + offA[1] + i * 2048);
+        fb[1][i] = *(const half8*)(cur + offB[1] + i * 2048);
+      }
+      __builtin_amdgcn_s_setprio(0);
+      // K-tile t + 1 landed (the only LDS-DMA in flight, plus the last epilogue's stores when
+      // one ran since: they are younger; waiting for at most 63 outstanding is still enough);
+      // every wave is done reading K-tile t
+      if (__builtin_expect(!post, 1)) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      } else if (st_full) {
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(ST_WAIT) : "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      post = false;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      // half 1 on R1; R0 <- K-tile t + 1's half 0 (stale data past the stream's end, unused);
+      // K-tile t + 2's LDS-DMA into this K-tile's buffer, two pieces per row block
+      const bool more = t + 2 < total;
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        mfma_row(1, i);
+        fa[0][i] = *(const half8*)(nxt + offA[0] + i * 2048);
+        fb[0][i] = *(const half8*)(nxt + offB[0] + i * 2048);
+        if (more) {
+          issue_piece(t + 2, 2 * i);
+          issue_piece(t + 2, 2 * i + 1);
+        }
+      }
+      __builtin_amdgcn_s_setprio(0);
+      if (more) advance_loader();
+    }
+    // the epilogue reads acc through VALU / accvgpr moves the hazard recognizer cannot relate to
+    // the asm MFMAs: let the last ones retire first
+    asm volatile("s_nop 15\n\ts_nop 3" ::: "memory");
+    // epilogue: row m0 + 128 wr + 16 i + fr, columns n0 + 128 wc + 32 p + 8 fq + 0..7 from the
+    // block pair (2p, 2p + 1)
+    const int T = lo + sidx + tl * nbx;
+    const int tm = T / tiles_n;
+    const int m0 = tm * 256, n0 = (T - tm * tiles_n) * 256;
+    post = true;
+    st_full = m0 + 256 <= g.M;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int n = n0 + 128 * wc + 32 * p + 8 * fq;
+      float bn[8];
+#pragma unroll
+      for (int r = 0; r < 8; ++r) bn[r] = sbias[n + r];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int m = m0 + 128 * wr + 16 * i + fr;
+        if (m < g.M) gemm_store8<EPI>(g, m, n, acc[i][2 * p], acc[i][2 * p + 1], bn);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // K2: LayerNorm over rows of D <= 1024 (one wave per row, two-pass mean/var in f32).
 // Optional row gather (pooling), f32 and/or f16 outputs (in-place f32 allowed).
 __global__ __launch_bounds__(256) void layernorm_kernel(LayerNormArgs a) {
@@ -1376,12 +1604,40 @@ int launch_gemm_8p_cfg(const GemmArgs& g, int epi, hipStream_t s) {
   return MRAG_OK;
 }
 
+// K3e (4 waves of 128 x 128) instead of K3d where both apply: env MRAG_GEMM_4W=1 (A/B timing)
+int gemm_4w_mode() {
+  static const int v = [] {
+    const char* e = getenv("MRAG_GEMM_4W");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
+int launch_gemm_4w(const GemmArgs& g, int epi, hipStream_t s) {
+  const int ntiles = ((g.M + 255) / 256) * (g.N / 256);
+  const dim3 grid((unsigned)std::min((ntiles + 7) / 8 * 8, std::max(8, num_cus() / 8 * 8)));
+  switch (epi) {
+    case EPI_F16: hipLaunchKernelGGL(gemm_4w_kernel<EPI_F16>, grid, dim3(G4_THREADS), 0, s, g); break;
+    case EPI_F16_QUICK_GELU: hipLaunchKernelGGL(gemm_4w_kernel<EPI_F16_QUICK_GELU>, grid, dim3(G4_THREADS), 0, s, g); break;
+    case EPI_F16_GELU_ERF: hipLaunchKernelGGL(gemm_4w_kernel<EPI_F16_GELU_ERF>, grid, dim3(G4_THREADS), 0, s, g); break;
+    case EPI_F32_RESIDUAL: hipLaunchKernelGGL(gemm_4w_kernel<EPI_F32_RESIDUAL>, grid, dim3(G4_THREADS), 0, s, g); break;
+    case EPI_F32: hipLaunchKernelGGL(gemm_4w_kernel<EPI_F32>, grid, dim3(G4_THREADS), 0, s, g); break;
+    default: return mrag::fail(MRAG_ERR_ARG, "gemm: bad epilogue %d", epi);
+  }
+  MRAG_CHECK_LAUNCH();
+  return MRAG_OK;
+}
+
 int launch_gemm(const GemmArgs& g, int epi, hipStream_t s) {
   if (g.M <= 0) return MRAG_OK;
   MRAG_REQUIRE(g.N % GN == 0 && g.K % GK == 0, "gemm: N=%d must be a multiple of %d and K=%d of %d", g.N, GN, g.K,
                GK);
   MRAG_REQUIRE(g.lda % 8 == 0 && g.ldw % 8 == 0 && g.ldc % 4 == 0, "gemm: lda/ldw must be multiples of 8, ldc of 4");
   if (gemm_big_mode() != 0 && g.M >= 1024 && g.N <= G8_BIAS_MAX && !k3_beats_k3d(g)) {
+    // K3e needs 32-bit byte offsets into A and W (SADDR LDS-DMA)
+    if (gemm_4w_mode() == 1 && g.N % 256 == 0 && (long)g.M * g.lda * 2 < (1l << 31) &&
+        (long)g.N * g.ldw * 2 < (1l << 31))
+      return launch_gemm_4w(g, epi, s);
     const int cfg = g8_pick_cfg(g);
     if (cfg == 0) return launch_gemm_8p_cfg<0>(g, epi, s);
     if (cfg == 1) return launch_gemm_8p_cfg<1>(g, epi, s);
