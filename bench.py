@@ -326,19 +326,45 @@ def fusion_leg(world: int, rank: int, local: int, steps: int, warmup: int):
         dist.all_gather_into_tensor(out, buf)
         return out[:NQ]
 
+    # the leg runs on its own stream: device-pointer encoder calls are then stream-ordered
+    # (no host sync per call; on the default stream the library synchronises every call). The
+    # text branch (MiniLM -> text search) and the image branch (CLIP text -> image search) are
+    # independent until the fusion; on one GPU the image branch runs in a second host thread
+    # on a second stream (a search returns to the host once its certificate is read, which
+    # would otherwise serialise the branches), so each branch's kernels that leave CUs idle
+    # (attention, LayerNorm, K8, partial GEMM rounds) overlap with the other's. At N > 1 the
+    # branches stay in one thread: their collectives share one communicator and must be issued
+    # in the same order on every rank. MRAG_FUSION_STREAMS=1 serialises them (A/B timing).
+    leg_stream = torch.cuda.Stream(device=dev)
+    two = world == 1 and os.environ.get("MRAG_FUSION_STREAMS", "2") != "1"
+    img_stream = torch.cuda.Stream(device=dev) if two else leg_stream
+    pool = None
+    if two:
+        from concurrent.futures import ThreadPoolExecutor
+
+        pool = ThreadPoolExecutor(max_workers=1)
+
+    def image_branch():
+        with torch.cuda.stream(img_stream):
+            iv = gather(clipt.embed_tokens(ids_c[lo:hi]))
+            return img_sh.search(iv, ki)
+
     def step():
+        if pool is not None:
+            img_stream.wait_stream(leg_stream)  # the previous step's fusion read its outputs
+            fut = pool.submit(image_branch)
+        else:
+            si, ri = image_branch()
         tv = gather(minilm.embed_tokens(ids_m[lo:hi], mask[lo:hi]))
-        iv = gather(clipt.embed_tokens(ids_c[lo:hi]))
         st, rt = text_sh.search(tv, kt)
-        si, ri = img_sh.search(iv, ki)
+        if pool is not None:
+            si, ri = fut.result()
+            leg_stream.wait_stream(img_stream)
         if rank == 0:
             pick, _ = fuse_scores_gpu(st, si, final_n)
             return pick.cpu()
         return None
 
-    # the leg runs on its own stream: device-pointer encoder calls are then stream-ordered
-    # (no host sync per call; on the default stream the library synchronises every call)
-    leg_stream = torch.cuda.Stream(device=dev)
     torch.cuda.synchronize()
     with torch.cuda.stream(leg_stream):
         for _ in range(warmup):
@@ -352,6 +378,8 @@ def fusion_leg(world: int, rank: int, local: int, steps: int, warmup: int):
         torch.cuda.synchronize()
         _barrier(world)
         dt = _max_over_ranks(time.perf_counter() - t0, world)
+    if pool is not None:
+        pool.shutdown()
     if rank != 0:
         return None
     fl = fusion_flops_per_query(world)

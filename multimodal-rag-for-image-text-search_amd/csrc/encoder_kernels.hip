@@ -839,39 +839,64 @@ __global__ __launch_bounds__(256) void layernorm_kernel(LayerNormArgs a) {
 
 // K2, vectorised (D % 4 == 0, 16-byte aligned rows: every encoder here): one wave per row,
 // lane l owns the float4 chunks l, l + 64, ... (16-byte loads, 16-byte f32 / 8-byte f16
-// stores); two-pass mean / variance in f32 from registers: one HBM pass over the row.
+// stores). Mean and variance in ONE butterfly: every lane takes the exact two-pass mean and
+// sum of squared deviations of its own <= 16 elements, and the butterfly merges (count, mean,
+// M2) pairwise (Chan et al.: delta = mb - ma, mean += delta nb / n, M2 += M2b + delta^2 na nb / n),
+// which is as well conditioned as the two-pass form; lane 0's result is used by all lanes.
+// gamma / beta are loaded before it: a wave's latency chain is one load, six shuffle rounds and
+// one store instead of two dependent reductions.
 __device__ __forceinline__ void ln_row4(f32x4 (&v)[4], int lane, int D, float eps, const float* gamma,
                                         const float* beta, float* y32, _Float16* y16) {
   typedef _Float16 half4 __attribute__((ext_vector_type(4)));
   const int nc = D >> 2;  // <= 256 chunks
-  float s = 0.f;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) s += (v[j][0] + v[j][1]) + (v[j][2] + v[j][3]);  // v = 0 past the row
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
-  const float mean = s / (float)D;
-  float q = 0.f;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    if (lane + 64 * j < nc) {
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const float d = v[j][t] - mean;
-        q += d * d;
-      }
-    }
-  }
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) q += __shfl_xor(q, off);
-  const float rstd = rsqrtf(q / (float)D + eps);
+  f32x4 g4[4], b4[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int c = lane + 64 * j;
     if (c < nc) {
-      const f32x4 g4 = ((const f32x4*)gamma)[c], b4 = ((const f32x4*)beta)[c];
+      g4[j] = ((const f32x4*)gamma)[c];
+      b4[j] = ((const f32x4*)beta)[c];
+    }
+  }
+  float cnt = 0.f, ls = 0.f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    if (lane + 64 * j < nc) {
+      cnt += 4.f;
+      ls += (v[j][0] + v[j][1]) + (v[j][2] + v[j][3]);
+    }
+  float mean = cnt > 0.f ? ls / cnt : 0.f, m2 = 0.f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    if (lane + 64 * j < nc) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const float d = v[j][t] - mean;
+        m2 += d * d;
+      }
+    }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const float nb = __shfl_xor(cnt, off), mb = __shfl_xor(mean, off), m2b = __shfl_xor(m2, off);
+    const float n = cnt + nb;
+    if (n > 0.f) {
+      const float delta = mb - mean;
+      mean += delta * (nb / n);
+      m2 += m2b + delta * delta * (cnt * nb / n);
+    }
+    cnt = n;
+  }
+  mean = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, mean)));
+  m2 = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, m2)));
+  const float var = m2 / (float)D;
+  const float rstd = rsqrtf(var + eps);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int c = lane + 64 * j;
+    if (c < nc) {
       f32x4 y;
 #pragma unroll
-      for (int t = 0; t < 4; ++t) y[t] = (v[j][t] - mean) * rstd * g4[t] + b4[t];
+      for (int t = 0; t < 4; ++t) y[t] = (v[j][t] - mean) * rstd * g4[j][t] + b4[j][t];
       if (y32) ((f32x4*)y32)[c] = y;
       if (y16) {
         half4 h;
@@ -1443,20 +1468,30 @@ __global__ void vit_assemble_kernel(const float* __restrict__ patch, const float
 }
 
 // Token embeddings: X[b*T+t] = tok[ids] + pos[t] (+ type0 for BERT)   (f32)
-__global__ void token_embed_kernel(const int32_t* __restrict__ ids, const float* __restrict__ tok,
-                                   const float* __restrict__ pos, const float* __restrict__ type_tab,
-                                   const int32_t* __restrict__ types, float* __restrict__ X, int B, int T, int D,
-                                   int vocab) {
-  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= (int64_t)B * T * D) return;
-  const int d = (int)(idx % D);
-  const int64_t bt = idx / D;
-  const int t = (int)(bt % T);
+// one workgroup per token row (float4 over D): X[bt] = tok[id] + pos[t] (+ type row)
+__global__ __launch_bounds__(128) void token_embed_kernel(const int32_t* __restrict__ ids, const float* __restrict__ tok,
+                                                          const float* __restrict__ pos, const float* __restrict__ type_tab,
+                                                          const int32_t* __restrict__ types, float* __restrict__ X, int B,
+                                                          int T, int D, int vocab) {
+  const int bt = blockIdx.x;
+  const int t = bt % T;
   int id = ids[bt];
   id = id < 0 ? 0 : (id >= vocab ? vocab - 1 : id);
-  float e = tok[(size_t)id * D + d] + pos[(size_t)t * D + d];
-  if (type_tab) e += type_tab[(types ? (types[bt] != 0) : 0) * D + d];  // BERT type_vocab_size 2
-  X[idx] = e;
+  const f32x4* e = (const f32x4*)(tok + (size_t)id * D);
+  const f32x4* p = (const f32x4*)(pos + (size_t)t * D);
+  const f32x4* ty = type_tab ? (const f32x4*)(type_tab + (size_t)(types ? (types[bt] != 0) : 0) * D) : nullptr;
+  f32x4* o = (f32x4*)(X + (size_t)bt * D);
+  for (int c = threadIdx.x; c < (D >> 2); c += blockDim.x) {
+    f32x4 v = e[c], q = p[c];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] += q[u];
+    if (ty) {  // BERT type_vocab_size 2
+      const f32x4 w = ty[c];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] += w[u];
+    }
+    o[c] = v;
+  }
 }
 
 // CLIP text pooling row per sequence: first index of eos_id (eos_id >= 0) or argmax of
@@ -1773,10 +1808,11 @@ int launch_vit_assemble(const float* patch, const float* cls, const float* pos, 
 
 int launch_token_embed(const int32_t* ids, const float* tok, const float* pos, const float* type_tab,
                        const int32_t* types, float* X, int B, int T, int D, int vocab, hipStream_t s) {
-  const int64_t n = (int64_t)B * T * D;
-  if (n == 0) return MRAG_OK;
-  hipLaunchKernelGGL(token_embed_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, ids, tok, pos, type_tab,
-                     types, X, B, T, D, vocab);
+  const int64_t n = (int64_t)B * T;
+  if (n == 0 || D == 0) return MRAG_OK;
+  MRAG_REQUIRE(D % 4 == 0 && n < (1ll << 31), "token_embed: D=%d must be a multiple of 4", D);
+  hipLaunchKernelGGL(token_embed_kernel, dim3((unsigned)n), dim3(128), 0, s, ids, tok, pos, type_tab, types, X, B, T,
+                     D, vocab);
   MRAG_CHECK_LAUNCH();
   return MRAG_OK;
 }

@@ -12,9 +12,8 @@
 // pairwise summation (leaves of <= 128 elements with 8 strided accumulators, halves split at
 // n/2 rounded down to a multiple of 8; the same order as K6, l2norm.hip); mean = sum / n and
 // var = sum((x - mean)^2) / n with every product, difference and partial sum rounded to f32
-// (no FMA contraction), std = correctly rounded f32 sqrt. One thread per query: the lists are
-// short (default 50 + 12) and the whole batch is a few microseconds, which removes the host
-// fusion (~5 ms per 1000 queries in numpy) from the config-5 step.
+// (no FMA contraction), std = correctly rounded f32 sqrt. One wave per query (see the kernel),
+// which removes the host fusion (~5 ms per 1000 queries in numpy) from the config-5 step.
 #include "common.h"
 
 namespace {
@@ -112,22 +111,34 @@ __device__ void np_mean_std(const Hits& h, int n, double& mean, double& std) {
   std = (double)(float)sqrt((double)v);
 }
 
-__global__ __launch_bounds__(64) void fuse_kernel(const float* __restrict__ ts, int kt, const float* __restrict__ is,
-                                                  int ki, int64_t nq, int final_n, int64_t* __restrict__ pick,
-                                                  double* __restrict__ combined) {
-  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (q >= nq) return;
+// One wave per query: lane 0 reproduces numpy's mean / std (serial pairwise order, a few
+// hundred dependent adds), every lane computes the z of its items, and the stable top-final_n
+// is final_n wave-wide (max z, min position) reductions — no per-thread scans of the list.
+__global__ __launch_bounds__(256) void fuse_kernel(const float* __restrict__ ts, int kt, const float* __restrict__ is,
+                                                   int ki, int64_t nq, int final_n, int64_t* __restrict__ pick,
+                                                   double* __restrict__ combined) {
+  const int lane = threadIdx.x & 63;
+  const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (q >= nq) return;  // whole wave
   const Hits th{ts + q * kt}, ih{is + q * ki};
   int nt = 0, ni = 0;  // valid hits (finite scores) form the prefix of each list
-  for (int i = 0; i < kt; ++i) nt += isfinite(th.s[i]) ? 1 : 0;
-  for (int i = 0; i < ki; ++i) ni += isfinite(ih.s[i]) ? 1 : 0;
-  double mt = 0, sdt = 0, mi = 0, sdi = 0;
-  if (nt) np_mean_std(th, nt, mt, sdt);
-  if (ni) np_mean_std(ih, ni, mi, sdi);
+  for (int b = 0; b < kt; b += 64) nt += __popcll(__ballot(b + lane < kt && isfinite(th.s[b + lane])));
+  for (int b = 0; b < ki; b += 64) ni += __popcll(__ballot(b + lane < ki && isfinite(ih.s[b + lane])));
+  double st[4] = {0, 0, 0, 0};  // text mean, std, image mean, std
+  if (lane == 0) {
+    if (nt) np_mean_std(th, nt, st[0], st[1]);
+    if (ni) np_mean_std(ih, ni, st[2], st[3]);
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int64_t bits = __shfl(__double_as_longlong(st[i]), 0);
+    st[i] = __longlong_as_double(bits);
+  }
+  const int n = nt + ni;
   auto z = [&](int c) -> double {  // combined score of concatenated item c (c < nt + ni)
-    if (c < nt) return sdt == 0.0 ? 0.0 : (th.s64(c) - mt) / sdt;
+    if (c < nt) return st[1] == 0.0 ? 0.0 : (th.s64(c) - st[0]) / st[1];
     const int j = c - nt;
-    return sdi == 0.0 ? 0.0 : (ih.s64(j) - mi) / sdi;
+    return st[3] == 0.0 ? 0.0 : (ih.s64(j) - st[2]) / st[3];
   };
   // stable descending sort, first final_n: repeated "best after the previous pick" under
   // (combined desc, position asc); positions index the concatenated [text kt | image ki] list
@@ -136,22 +147,34 @@ __global__ __launch_bounds__(64) void fuse_kernel(const float* __restrict__ ts, 
   for (int slot = 0; slot < final_n; ++slot) {
     double bz = -INFINITY;
     int bc = -1;
-    for (int c = 0; c < nt + ni; ++c) {
+    for (int c = lane; c < n; c += 64) {
       const double zc = z(c);
       const bool after = pc < 0 || zc < pz || (zc == pz && c > pc);
-      if (after && (bc < 0 || zc > bz)) {
+      if (after && (bc < 0 || zc > bz)) {  // c ascends per lane: ties keep the first
         bz = zc;
         bc = c;
       }
     }
-    const size_t o = (size_t)q * final_n + slot;
-    if (bc < 0) {
-      pick[o] = -1;
-      combined[o] = NAN;
-      continue;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      const double oz = __longlong_as_double(__shfl_xor(__double_as_longlong(bz), off));
+      const int oc = __shfl_xor(bc, off);
+      if (oc >= 0 && (bc < 0 || oz > bz || (oz == bz && oc < bc))) {
+        bz = oz;
+        bc = oc;
+      }
     }
-    pick[o] = bc < nt ? bc : kt + (bc - nt);
-    combined[o] = bz;
+    if (bc < 0) {  // fewer than final_n hits: the rest of the row is padding
+      for (int r = slot + lane; r < final_n; r += 64) {
+        pick[(size_t)q * final_n + r] = -1;
+        combined[(size_t)q * final_n + r] = NAN;
+      }
+      break;
+    }
+    if (lane == 0) {
+      pick[(size_t)q * final_n + slot] = bc < nt ? bc : kt + (bc - nt);
+      combined[(size_t)q * final_n + slot] = bz;
+    }
     pz = bz;
     pc = bc;
   }
@@ -166,7 +189,7 @@ extern "C" int mrag_fuse_scores(const float* text_scores, int32_t kt, const floa
   if (nq == 0 || final_n == 0) return MRAG_OK;
   MRAG_REQUIRE(pick && combined && (kt == 0 || text_scores) && (ki == 0 || image_scores), "NULL pointer");
   MRAG_REQUIRE(nq < (1ll << 30), "too many queries");
-  hipLaunchKernelGGL(fuse_kernel, dim3((unsigned)((nq + 63) / 64)), dim3(64), 0, (hipStream_t)stream, text_scores,
+  hipLaunchKernelGGL(fuse_kernel, dim3((unsigned)((nq + 3) / 4)), dim3(256), 0, (hipStream_t)stream, text_scores,
                      kt, image_scores, ki, nq, final_n, pick, combined);
   MRAG_CHECK_LAUNCH();
   return MRAG_OK;

@@ -118,6 +118,93 @@ __device__ float combine(const float* leaf, int off, int n, int& li) {
   return __fadd_rn(a, b);
 }
 
+// Compile-time leaf table and combination tree for the encoder widths (no runtime recursion:
+// the generic path below compiles to calls with a scratch stack).
+struct LeafTab {
+  int n;
+  int off[8], len[8];
+};
+constexpr void leaves_rec(LeafTab& t, int off, int n) {
+  if (n <= 128) {
+    t.off[t.n] = off;
+    t.len[t.n] = n;
+    ++t.n;
+    return;
+  }
+  int n2 = n / 2;
+  n2 -= n2 % 8;
+  leaves_rec(t, off, n2);
+  leaves_rec(t, off + n2, n - n2);
+}
+constexpr LeafTab leaves_for(int dim) {
+  LeafTab t{};
+  leaves_rec(t, 0, dim);
+  return t;
+}
+constexpr bool leaves_whole_octets(int dim) {  // every leaf a multiple of 8, >= 8 (no tails)
+  const LeafTab t = leaves_for(dim);
+  for (int i = 0; i < t.n; ++i)
+    if (t.len[i] < 8 || t.len[i] % 8) return false;
+  return true;
+}
+constexpr int leaf_at(const LeafTab& t, int off) {
+  for (int i = 0; i < t.n; ++i)
+    if (t.off[i] == off) return i;
+  return -1;
+}
+template <int DIM, int OFF, int N>
+__device__ __forceinline__ float combine_ct(const float (&lv)[8]) {
+  if constexpr (N <= 128) {
+    constexpr int i = leaf_at(leaves_for(DIM), OFF);
+    static_assert(i >= 0, "leaf table");
+    return lv[i];
+  } else {
+    constexpr int N2 = N / 2 - (N / 2) % 8;
+    return __fadd_rn(combine_ct<DIM, OFF, N2>(lv), combine_ct<DIM, OFF + N2, N - N2>(lv));
+  }
+}
+
+// One wave per row, DIM known at compile time (128 < DIM <= 1024, DIM % 8 == 0: every
+// leaf is 64..128 elements, a multiple of 8). Lane 8 leaf + j owns accumulator j of leaf
+// `leaf`; the leaf value ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)) and the tree follow numpy.
+template <int DIM>
+__global__ __launch_bounds__(256) void l2norm_rows_ct_kernel(const float* x, float* y, int64_t rows) {
+  constexpr LeafTab L = leaves_for(DIM);
+  static_assert(L.n <= 8 && leaves_whole_octets(DIM), "<= 8 leaves, no leaf tails");
+  const int lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= rows) return;
+  const float* xr = x + r * DIM;
+  float* yr = y + r * DIM;
+  const int leaf = lane >> 3, j = lane & 7;
+  float acc = 0.f;
+  int loff = 0, llen = 0;
+#pragma unroll
+  for (int q = 0; q < 8; ++q)
+    if (q == leaf && q < L.n) {
+      loff = L.off[q];
+      llen = L.len[q];
+    }
+  if (llen) {
+    const float* p = xr + loff;
+    acc = __fmul_rn(p[j], p[j]);
+    for (int i = j + 8; i < llen; i += 8) acc = __fadd_rn(acc, __fmul_rn(p[i], p[i]));
+  }
+  const int b = lane & ~7;
+  float rr[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) rr[q] = __shfl(acc, b + q);
+  const float lv0 = __fadd_rn(__fadd_rn(__fadd_rn(rr[0], rr[1]), __fadd_rn(rr[2], rr[3])),
+                              __fadd_rn(__fadd_rn(rr[4], rr[5]), __fadd_rn(rr[6], rr[7])));
+  float lv[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) lv[q] = __shfl(lv0, 8 * q);
+  const float ss = combine_ct<DIM, 0, DIM>(lv);
+  float nrm = (float)sqrt((double)ss);  // correctly rounded f32 sqrt (see the generic kernel)
+  if (nrm == 0.0f) nrm = 1.0f;
+  for (int d = lane; d < DIM; d += 64) yr[d] = __fdiv_rn(xr[d], nrm);  // IEEE f32 division = numpy's
+}
+
 // One wave per row. Lane 8*leaf + j owns accumulator j of leaf `leaf` (numpy keeps 8
 // strided accumulators per leaf); leaf and tree combinations follow numpy's order exactly.
 __global__ __launch_bounds__(256) void l2norm_rows_wave_kernel(const float* x, float* y,  // may alias
@@ -185,7 +272,12 @@ extern "C" int mrag_l2norm_rows(const float* x, float* y, int64_t rows, int32_t 
   MRAG_REQUIRE(dim <= (1 << 20), "dim %d too large", dim);
   if (rows == 0) return MRAG_OK;
   MRAG_REQUIRE(x != nullptr && y != nullptr, "NULL pointer");
-  if (dim <= 968) {  // wave per row: numpy splits dims <= 968 into <= 8 leaves of <= 128
+  if (dim == 384 || dim == 512 || dim == 768) {  // the encoders' widths: compile-time tree
+    const int64_t blocks = (rows + 3) / 4;
+    MRAG_REQUIRE(blocks < (1ll << 31), "too many rows");
+    auto k = dim == 384 ? l2norm_rows_ct_kernel<384> : dim == 512 ? l2norm_rows_ct_kernel<512> : l2norm_rows_ct_kernel<768>;
+    hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, x, y, rows);
+  } else if (dim <= 968) {  // wave per row: numpy splits dims <= 968 into <= 8 leaves of <= 128
     const int64_t blocks = (rows + 3) / 4;
     MRAG_REQUIRE(blocks < (1ll << 31), "too many rows");
     hipLaunchKernelGGL(l2norm_rows_wave_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, x, y,
