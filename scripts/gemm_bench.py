@@ -25,6 +25,11 @@ SHAPES = {  # name: (M, N, K, epilogue)
     "t_out": (16000, 512, 512, 3),
     "t_fc1": (16000, 2048, 512, 1),
     "t_fc2": (16000, 512, 2048, 3),
+    # MiniLM at the config-5 batch
+    "m_qkv": (16000, 1152, 384, 0),
+    "m_out": (16000, 384, 384, 3),
+    "m_fc1": (16000, 1536, 384, 2),
+    "m_fc2": (16000, 384, 1536, 3),
 }
 
 

@@ -12,7 +12,8 @@ import torch  # noqa: E402
 from app.encoders import gemm_nt  # noqa: E402
 
 CASES = [(12800, 2304, 768, 0), (12800, 3072, 768, 1), (12800, 768, 3072, 3), (12800, 768, 768, 3),
-         (12850, 768, 768, 4), (4000, 1536, 512, 2), (1100, 512, 2048, 3), (2560, 1024, 64, 0), (1030, 256, 128, 1)]
+         (12850, 768, 768, 4), (4000, 1536, 512, 2), (1100, 512, 2048, 3), (2560, 1024, 64, 0), (1030, 256, 128, 1),
+         (16000, 512, 512, 3), (16000, 512, 2048, 3), (16000, 2048, 512, 1)]
 out = {}
 for ci, (M, N, K, epi) in enumerate(CASES):
     g = torch.Generator(device="cuda").manual_seed(ci)
