@@ -49,9 +49,9 @@ class ShardedFlatIndex:
 
     def search(self, queries, k: int, label: int = -1) -> Tuple:
         """(scores f32 [nq,k], rows int64 [nq,k]) over the whole sharded corpus."""
-        s, r, s64 = self.local.search(queries, k, label=label, row_offset=self.row_offset, with_f64=True)
         if self.world == 1:
-            return s, r
+            return self.local.search(queries, k, label=label, row_offset=self.row_offset)
+        s, r, s64 = self.local.search(queries, k, label=label, row_offset=self.row_offset, with_f64=True)
         ms, mr, _ = self._merge(self._gather(s64), self._gather(r), k)
         return ms, mr
 

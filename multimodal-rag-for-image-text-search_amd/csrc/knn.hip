@@ -2021,14 +2021,27 @@ __global__ __launch_bounds__(MERGE_THREADS) void topk_merge_kernel(const double*
 
 // Row preparation: in f32 [nin][D] -> x32 [nout][DP] (zero padded), |x| f64,
 // x16 = fp16(x/|x|). One wave per row.
+// Per-search scratch cleared by the query prep (instead of three memset launches): the
+// certificate counters, the per-slot collect counts and the shared thresholds.
+struct PrepClear {
+  int32_t* counters;  // [4] or null
+  int32_t* cand_cnt;  // [nout] or null
+  uint32_t* theta;    // [nout] or null
+};
+
 __global__ __launch_bounds__(256) void prep_rows_kernel(const float* __restrict__ in, int64_t nin,
                                                         int D, int DP, int64_t nout,
                                                         float* __restrict__ x32,
                                                         double* __restrict__ xn,
-                                                        _Float16* __restrict__ x16) {
+                                                        _Float16* __restrict__ x16, PrepClear clr) {
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (clr.counters && blockIdx.x == 0 && threadIdx.x < 4) clr.counters[threadIdx.x] = 0;
   if (row >= nout) return;
+  if (lane == 0) {
+    if (clr.cand_cnt) clr.cand_cnt[row] = 0;
+    if (clr.theta) clr.theta[row] = 0u;
+  }
   float v[8];
   double ss = 0.0;
 #pragma unroll
@@ -2078,11 +2091,11 @@ __global__ __launch_bounds__(256) void prep_rows_wide_kernel(const float* __rest
 }
 
 int launch_prep(const float* in, int64_t nin, int D, int DP, int64_t nout, float* x32, double* xn, _Float16* x16,
-                hipStream_t s) {
+                hipStream_t s, PrepClear clr = PrepClear{}) {
   if (nout <= 0) return MRAG_OK;
   if (DP <= 512)
     hipLaunchKernelGGL(prep_rows_kernel, dim3((unsigned)((nout + 3) / 4)), dim3(256), 0, s, in, nin, D, DP, nout,
-                       x32, xn, x16);
+                       x32, xn, x16, clr);
   else
     hipLaunchKernelGGL(prep_rows_wide_kernel, dim3((unsigned)((nout + 3) / 4)), dim3(256), 0, s, in, nin, D, DP,
                        nout, x32, xn, x16);
@@ -2251,6 +2264,7 @@ struct mrag_knn_index {
   bool scan_v4 = false;    // env MRAG_SCAN_V4=1: the two-waves-per-SIMD v4 scan instead of v3 (A/B timing)
   bool scan_v5 = false;    // env MRAG_SCAN_V5=1: the three-buffer 48-row v5 scan instead of v3
   int32_t* host_counters = nullptr;  // pinned [2]: fail_cnt, overflow
+  hipEvent_t done = nullptr;         // end of a search's device work (waited by spinning)
   mrag_knn::Workspace gws[8];  // K7g buffers
   int64_t last_uncertified = 0, last_retries = 0;
   // optional scan timing (mrag_knn_profile)
@@ -2261,6 +2275,20 @@ struct mrag_knn_index {
 };
 
 namespace {
+
+// Block until everything enqueued on s so far has run: an event recorded behind it, polled.
+// The search's answer depends on the certificate counters it reads back, so a search returns
+// only once its device work is done; polling wakes the host within a microsecond or two of the
+// last kernel, where a stream synchronize could leave the GPU idle for tens of microseconds
+// between back-to-back searches.
+int wait_stream(mrag_knn_index* ix, hipStream_t s) {
+  MRAG_HIP(hipEventRecord(ix->done, s));
+  hipError_t e;
+  while ((e = hipEventQuery(ix->done)) == hipErrorNotReady) {
+  }
+  if (e != hipSuccess) return mrag::fail(MRAG_ERR_HIP, "search: %s", hipGetErrorString(e));
+  return MRAG_OK;
+}
 
 int grow(mrag_knn_index* ix, int64_t need) {
   if (need <= ix->cap) return MRAG_OK;
@@ -2322,6 +2350,7 @@ int mrag_knn_create(int32_t dim, int32_t device, mrag_knn_index** out) {
   if (const char* v5 = getenv("MRAG_SCAN_V5")) ix->scan_v5 = atoi(v5) != 0;
   hipError_t e = hipStreamCreateWithFlags(&ix->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipHostMalloc((void**)&ix->host_counters, 16, hipHostMallocDefault);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&ix->done, hipEventDisableTiming);
   if (e != hipSuccess) {
     delete ix;
     return mrag::fail(MRAG_ERR_HIP, "stream/pinned alloc: %s", hipGetErrorString(e));
@@ -2342,6 +2371,7 @@ int mrag_knn_destroy(mrag_knn_index* ix) {
       release(*b);
     mrag_knn::release(ix->gws);
     if (ix->host_counters) (void)hipHostFree(ix->host_counters);
+    if (ix->done) (void)hipEventDestroy(ix->done);
     if (ix->ev0) (void)hipEventDestroy(ix->ev0);
     if (ix->ev1) (void)hipEventDestroy(ix->ev1);
     if (ix->stream) (void)hipStreamDestroy(ix->stream);
@@ -2551,11 +2581,9 @@ int mrag_knn_search(mrag_knn_index* ix, const float* queries, int64_t nq, int32_
     if (use_v3)
       if (int rc = ensure(ix->part_tau, (size_t)S * Qp * 4)) return rc;
 
-    if (int rc = launch_prep(qsrc, nq, D, DP, Qp, (float*)ix->q32.p, (double*)ix->qn.p, (_Float16*)ix->q16.p, s))
+    if (int rc = launch_prep(qsrc, nq, D, DP, Qp, (float*)ix->q32.p, (double*)ix->qn.p, (_Float16*)ix->q16.p, s,
+                             PrepClear{(int32_t*)ix->counters.p, (int32_t*)ix->cand_cnt.p, (uint32_t*)ix->theta.p}))
       return rc;
-    MRAG_HIP(hipMemsetAsync(ix->counters.p, 0, 16, s));
-    MRAG_HIP(hipMemsetAsync(ix->cand_cnt.p, 0, (size_t)Qp * 4, s));
-    MRAG_HIP(hipMemsetAsync(ix->theta.p, 0, (size_t)Qp * 4, s));
 
     ScanParams sp{};
     sp.theta = (uint32_t*)ix->theta.p;
@@ -2698,7 +2726,7 @@ int mrag_knn_search(mrag_knn_index* ix, const float* queries, int64_t nq, int32_
       hipLaunchKernelGGL(knn_final_kernel, dim3((unsigned)nq), dim3(MERGE_THREADS), (size_t)DP * 4, s, fp);
       MRAG_CHECK_LAUNCH();
       MRAG_HIP(hipMemcpyAsync(ix->host_counters, ix->counters.p, 8, hipMemcpyDeviceToHost, s));
-      MRAG_HIP(hipStreamSynchronize(s));
+      if (int rc = wait_stream(ix, s)) return rc;
       ix->last_uncertified = ix->host_counters[0];
       if (ix->profile) {
         float ms = 0.f;
@@ -2718,8 +2746,7 @@ int mrag_knn_search(mrag_knn_index* ix, const float* queries, int64_t nq, int32_
     MRAG_HIP(hipMemcpyAsync(out_rows, orr, nout * 8, hipMemcpyDeviceToHost, s));
     if (out_scores64) MRAG_HIP(hipMemcpyAsync(out_scores64, os64, nout * 8, hipMemcpyDeviceToHost, s));
   }
-  MRAG_HIP(hipStreamSynchronize(s));
-  return MRAG_OK;
+  return wait_stream(ix, s);
 }
 
 int mrag_topk_merge(const double* scores64, const int64_t* rows, int32_t nlists, int64_t nq, int32_t k,
