@@ -1287,7 +1287,7 @@ __global__ __launch_bounds__(256) void attention_mfma64t_kernel(AttentionArgs a)
 // are skipped, and every other block is processed identically whatever the batch's length:
 // a sequence's result does not depend on how its batch is padded, for every L. Work per
 // (sequence, head) grows with its own length only, not with a 64-row pad.
-template <int DH>
+template <int DH, int PF = 1>  // PF 1: operands two key blocks ahead; 0: at the top of each block (A/B)
 __global__ __launch_bounds__(256) void attention_flash16_kernel(AttentionArgs a) {
   constexpr int KS = DH / 32;               // 32-dim k-steps of S^T
   constexpr int DB = DH / 16;               // 16-dim blocks of O^T
@@ -1315,39 +1315,62 @@ __global__ __launch_bounds__(256) void attention_flash16_kernel(AttentionArgs a)
   float m = -INFINITY, l = 0.f;
   _Float16* vs = Vs[w];
   const int nkb = a.causal ? min((L + 15) >> 4, qb + 1) : (L + 15) >> 4;
-  for (int kb = 0; kb < nkb; ++kb) {
+  // a key block's operands (K fragments, this lane's V chunks, its 4 keys' mask flags) are
+  // loaded two blocks ahead, so the per-block chain is compute only after the first block's
+  // load latency (it was K load -> MFMA -> V load -> LDS: two memory latencies per block)
+  struct Blk {
+    half8 kf[KS], vv[KS];
     bool kv[4];
-    bool any_ok = false;
+  };
+  auto load_blk = [&](int kb, Blk& x) {
+    const int krow = 16 * kb + c;
+#pragma unroll
+    for (int st = 0; st < KS; ++st)
+      x.kf[st] = krow < L ? *(const half8*)(base + (size_t)krow * rs + D + 32 * st + 8 * g) : half8{};
+#pragma unroll
+    for (int t = 0; t < KS; ++t) {
+      const int idx = lane + 64 * t, key = idx / (DH / 8), ch = idx % (DH / 8);
+      const int kr = 16 * kb + key;
+      x.vv[t] = kr < L ? *(const half8*)(base + (size_t)kr * rs + 2 * D + 8 * ch) : half8{};
+    }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int key = 16 * kb + 4 * g + r;
       bool ok = key < L;
       if (ok && a.mask) ok = a.mask[(size_t)b * L + key] != 0;
       if (a.causal) ok = ok && key <= qrow;
-      kv[r] = ok;
-      any_ok |= ok;
+      x.kv[r] = ok;
     }
-    if (!__any(any_ok)) continue;  // wave-uniform
-    const int krow = 16 * kb + c;
+  };
+  Blk cur, n1, n2;
+  if (PF && nkb > 0) load_blk(0, n1);
+  if (PF && nkb > 1) load_blk(1, n2);
+  for (int kb = 0; kb < nkb; ++kb) {
+    if constexpr (PF) {
+      cur = n1;
+      n1 = n2;
+      if (kb + 2 < nkb) load_blk(kb + 2, n2);
+    } else {
+      load_blk(kb, cur);
+    }
+    bool any_ok = false;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) any_ok |= cur.kv[r];
+    if (!__any(any_ok)) continue;  // wave-uniform: a fully masked key block
     f32x4 sacc = {};
 #pragma unroll
-    for (int st = 0; st < KS; ++st) {
-      const half8 kf = krow < L ? *(const half8*)(base + (size_t)krow * rs + D + 32 * st + 8 * g) : half8{};
-      sacc = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf, qf[st], sacc, 0, 0, 0);
-    }
+    for (int st = 0; st < KS; ++st) sacc = __builtin_amdgcn_mfma_f32_16x16x32_f16(cur.kf[st], qf[st], sacc, 0, 0, 0);
     // V rows of the block -> this wave's LDS image (16 B per lane per row chunk)
     asm volatile("" ::: "memory");  // the previous block's transposed reads come first
 #pragma unroll
     for (int t = 0; t < KS; ++t) {
       const int idx = lane + 64 * t, key = idx / (DH / 8), ch = idx % (DH / 8);
-      const int kr = 16 * kb + key;
-      const half8 v = kr < L ? *(const half8*)(base + (size_t)kr * rs + 2 * D + 8 * ch) : half8{};
-      *(half8*)(vs + key * VROW + 8 * ch) = v;
+      *(half8*)(vs + key * VROW + 8 * ch) = cur.vv[t];
     }
     float sv[4], bmax = -INFINITY;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      sv[r] = kv[r] ? sacc[r] * a.scale : -INFINITY;
+      sv[r] = cur.kv[r] ? sacc[r] * a.scale : -INFINITY;
       bmax = fmaxf(bmax, sv[r]);
     }
     bmax = fmaxf(bmax, __shfl_xor(bmax, 16));
@@ -1758,10 +1781,13 @@ int launch_attention(const AttentionArgs& a, int dh, hipStream_t s) {
     const int64_t items = (int64_t)a.B * a.H * ((a.L + 15) / 16);
     MRAG_REQUIRE(items < (1ll << 33), "attention: batch too large");
     const dim3 g4((unsigned)((items + 3) / 4));
-    if (dh == 64)
-      hipLaunchKernelGGL(attention_flash16_kernel<64>, g4, dim3(256), 0, s, a);
-    else
-      hipLaunchKernelGGL(attention_flash16_kernel<32>, g4, dim3(256), 0, s, a);
+    static const bool no_prefetch = [] {  // MRAG_ATTN_PREFETCH=0: operands loaded per block (A/B timing)
+      const char* e = getenv("MRAG_ATTN_PREFETCH");
+      return e && atoi(e) == 0;
+    }();
+    auto kern = dh == 64 ? (no_prefetch ? attention_flash16_kernel<64, 0> : attention_flash16_kernel<64, 1>)
+                         : (no_prefetch ? attention_flash16_kernel<32, 0> : attention_flash16_kernel<32, 1>);
+    hipLaunchKernelGGL(kern, g4, dim3(256), 0, s, a);
   } else if (dh == 64 && a.L <= 64 && !force_valu_attention() && !attn_v1) {
     hipLaunchKernelGGL(attention_mfma64t_kernel<64>, dim3((unsigned)((a.B * a.H + 3) / 4)), dim3(256), 0, s, a);
   } else if (dh == 32 && a.L <= 64 && mfma_attention_dh32()) {

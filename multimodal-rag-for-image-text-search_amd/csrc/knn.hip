@@ -1732,7 +1732,68 @@ __device__ __forceinline__ float f32_round_down(double x) {
   return f;
 }
 
+// Wave-level bitonic network on E = 64 P keys held P per lane (element e = 64 p + lane),
+// ascending. Stages with stride >= 64 swap registers within a lane, the others exchange with
+// lane ^ stride. (Network checked against a host emulation for P = 1, 2.)
+template <int P>
+__device__ __forceinline__ void wave_sort_keys(uint64_t (&k)[P], int lane) {
+  constexpr int E = 64 * P;
+#pragma unroll
+  for (int size = 2; size <= E; size <<= 1) {
+#pragma unroll
+    for (int st = size >> 1; st > 0; st >>= 1) {
+      if (st >= 64) {  // P == 2, st == 64: element p = 0 is the lower one; size = 128 is ascending
+        if constexpr (P == 2) {
+          const uint64_t a = k[0], b = k[1];
+          k[0] = a < b ? a : b;
+          k[1] = a < b ? b : a;
+        }
+      } else {
+#pragma unroll
+        for (int pp = 0; pp < P; ++pp) {
+          const int e = 64 * pp + lane;
+          const bool asc = (e & size) == 0, lower = (lane & st) == 0;
+          const uint64_t o = __shfl_xor((unsigned long long)k[pp], st);
+          const uint64_t lo = k[pp] < o ? k[pp] : o, hi = k[pp] < o ? o : k[pp];
+          k[pp] = (lower == asc) ? lo : hi;
+        }
+      }
+    }
+  }
+}
+// run <- the E smallest of run and b (both ascending), ascending: min(run[e], b[E-1-e]) is
+// bitonic, then one ascending half-cleaner cascade
+template <int P>
+__device__ __forceinline__ void wave_merge_lowest(uint64_t (&run)[P], const uint64_t (&b)[P], int lane) {
+#pragma unroll
+  for (int pp = 0; pp < P; ++pp) {
+    const uint64_t rb = __shfl((unsigned long long)b[P - 1 - pp], 63 - lane);
+    run[pp] = run[pp] < rb ? run[pp] : rb;
+  }
+#pragma unroll
+  for (int st = 32 * P; st > 0; st >>= 1) {
+    if (st >= 64) {
+      if constexpr (P == 2) {
+        const uint64_t a = run[0], c = run[1];
+        run[0] = a < c ? a : c;
+        run[1] = a < c ? c : a;
+      }
+    } else {
+#pragma unroll
+      for (int pp = 0; pp < P; ++pp) {
+        const uint64_t o = __shfl_xor((unsigned long long)run[pp], st);
+        const bool lower = (lane & st) == 0;
+        run[pp] = lower ? (run[pp] < o ? run[pp] : o) : (run[pp] < o ? o : run[pp]);
+      }
+    }
+  }
+}
+
 // K8: merge split lists, rescore exactly, certify. One workgroup per query.
+// SEL = 0: bitonic sort of all S KL keys in LDS. SEL = P > 0 (when M + 1 <= 64 P): only the
+// 64 P best keys are kept — every wave folds its share of the lists, 64 P keys at a time, into
+// a running top-64P in registers (wave-level bitonic, no barriers), then wave 0 merges the four.
+template <int SEL>
 __global__ __launch_bounds__(MERGE_THREADS) void knn_merge_kernel(MergeParams p) {
   extern __shared__ __attribute__((aligned(16))) char dsm[];
   uint64_t* keys = (uint64_t*)dsm;                                  // [R]
@@ -1748,7 +1809,7 @@ __global__ __launch_bounds__(MERGE_THREADS) void knn_merge_kernel(MergeParams p)
   float tau = -INFINITY;
   int valid = 0;
   const int ntot = p.splits * p.KL;
-  for (int e = tid; e < p.R; e += MERGE_THREADS) {
+  auto load_key = [&](int e) -> uint64_t {  // candidate e of the union; invalid -> ~0 (sorts last)
     uint64_t key = ~0ull;
     if (e < ntot) {
       const int sp = e / p.KL, j = e - sp * p.KL;
@@ -1761,7 +1822,24 @@ __global__ __launch_bounds__(MERGE_THREADS) void knn_merge_kernel(MergeParams p)
         if (j == p.KL - 1) tau = fmaxf(tau, s);
       }
     }
-    keys[e] = key;
+    return key;
+  };
+  if constexpr (SEL == 0) {
+    for (int e = tid; e < p.R; e += MERGE_THREADS) keys[e] = load_key(e);
+  } else {
+    constexpr int E = 64 * SEL;
+    uint64_t run[SEL];
+#pragma unroll
+    for (int pp = 0; pp < SEL; ++pp) run[pp] = ~0ull;
+    for (int c = wave; c * E < ntot; c += MERGE_THREADS / 64) {  // wave-uniform
+      uint64_t ch[SEL];
+#pragma unroll
+      for (int pp = 0; pp < SEL; ++pp) ch[pp] = load_key(c * E + 64 * pp + lane);
+      wave_sort_keys<SEL>(ch, lane);
+      wave_merge_lowest<SEL>(run, ch, lane);
+    }
+#pragma unroll
+    for (int pp = 0; pp < SEL; ++pp) keys[wave * E + 64 * pp + lane] = run[pp];
   }
   if (p.part_tau)
     for (int sp = tid; sp < p.splits; sp += MERGE_THREADS) tau = fmaxf(tau, p.part_tau[(size_t)sp * p.Qp + q]);
@@ -1783,20 +1861,36 @@ __global__ __launch_bounds__(MERGE_THREADS) void knn_merge_kernel(MergeParams p)
     valid += red_i[i];
   }
 
-  // bitonic sort of keys ascending == (approx desc, row asc)
-  for (int size = 2; size <= p.R; size <<= 1) {
-    for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      __syncthreads();
-      for (int i = tid; i < (p.R >> 1); i += MERGE_THREADS) {
-        const int lo = 2 * i - (i & (stride - 1));
-        const int hi = lo + stride;
-        const bool asc = (lo & size) == 0;
-        const uint64_t a = keys[lo], b = keys[hi];
-        if ((a > b) == asc) {
-          keys[lo] = b;
-          keys[hi] = a;
+  if constexpr (SEL == 0) {
+    // bitonic sort of keys ascending == (approx desc, row asc)
+    for (int size = 2; size <= p.R; size <<= 1) {
+      for (int stride = size >> 1; stride > 0; stride >>= 1) {
+        __syncthreads();
+        for (int i = tid; i < (p.R >> 1); i += MERGE_THREADS) {
+          const int lo = 2 * i - (i & (stride - 1));
+          const int hi = lo + stride;
+          const bool asc = (lo & size) == 0;
+          const uint64_t a = keys[lo], b = keys[hi];
+          if ((a > b) == asc) {
+            keys[lo] = b;
+            keys[hi] = a;
+          }
         }
       }
+    }
+  } else {  // wave 0 folds the other waves' top-E into its own; keys[0 .. E) = the E best
+    constexpr int E = 64 * SEL;
+    if (wave == 0) {
+      uint64_t run[SEL], other[SEL];
+#pragma unroll
+      for (int pp = 0; pp < SEL; ++pp) run[pp] = keys[64 * pp + lane];
+      for (int w2 = 1; w2 < MERGE_THREADS / 64; ++w2) {
+#pragma unroll
+        for (int pp = 0; pp < SEL; ++pp) other[pp] = keys[w2 * E + 64 * pp + lane];
+        wave_merge_lowest<SEL>(run, other, lane);
+      }
+#pragma unroll
+      for (int pp = 0; pp < SEL; ++pp) keys[64 * pp + lane] = run[pp];
     }
   }
   __syncthreads();
@@ -2688,8 +2782,18 @@ int mrag_knn_search(mrag_knn_index* ix, const float* queries, int64_t nq, int32_
     mp.fail_cnt = (int32_t*)ix->counters.p;
     mp.theta = (const uint32_t*)ix->theta.p;
     mp.part_tau = sp.part_tau;
-    const size_t msh = (size_t)R * 8 + (size_t)Mp * 12 + (size_t)DP * 4 + 64;
-    hipLaunchKernelGGL(knn_merge_kernel, dim3((unsigned)nq), dim3(MERGE_THREADS), msh, s, mp);
+    // K8 key selection: the best M + 1 keys (the M candidates and the first one left out) by
+    // the register top-64P fold when they fit, else the full bitonic sort (env MRAG_K8_SORT=1
+    // forces the sort: A/B timing)
+    static const bool k8_sort = [] {
+      const char* e = getenv("MRAG_K8_SORT");
+      return e && atoi(e) == 1;
+    }();
+    const int sel = k8_sort ? 0 : (M + 1 <= 64 ? 1 : (M + 1 <= 128 ? 2 : 0));
+    mp.R = sel ? std::max(R, 4 * 64 * sel) : R;  // the fold parks four waves' top-64P in keys[]
+    const size_t msh = (size_t)mp.R * 8 + (size_t)Mp * 12 + (size_t)DP * 4 + 64;
+    auto merge = sel == 1 ? knn_merge_kernel<1> : sel == 2 ? knn_merge_kernel<2> : knn_merge_kernel<0>;
+    hipLaunchKernelGGL(merge, dim3((unsigned)nq), dim3(MERGE_THREADS), msh, s, mp);
     MRAG_CHECK_LAUNCH();
 
     {
