@@ -839,64 +839,41 @@ __global__ __launch_bounds__(256) void layernorm_kernel(LayerNormArgs a) {
 
 // K2, vectorised (D % 4 == 0, 16-byte aligned rows: every encoder here): one wave per row,
 // lane l owns the float4 chunks l, l + 64, ... (16-byte loads, 16-byte f32 / 8-byte f16
-// stores). Mean and variance in ONE butterfly: every lane takes the exact two-pass mean and
-// sum of squared deviations of its own <= 16 elements, and the butterfly merges (count, mean,
-// M2) pairwise (Chan et al.: delta = mb - ma, mean += delta nb / n, M2 += M2b + delta^2 na nb / n),
-// which is as well conditioned as the two-pass form; lane 0's result is used by all lanes.
-// gamma / beta are loaded before it: a wave's latency chain is one load, six shuffle rounds and
-// one store instead of two dependent reductions.
+// stores); two-pass mean / variance in f32 from registers: one HBM pass over the row. (A
+// single butterfly merging per-lane (count, mean, M2) pairs measured slower: 16.2 vs 12.5 us
+// per ViT LayerNorm — three shuffles and a division per round.)
 __device__ __forceinline__ void ln_row4(f32x4 (&v)[4], int lane, int D, float eps, const float* gamma,
                                         const float* beta, float* y32, _Float16* y16) {
   typedef _Float16 half4 __attribute__((ext_vector_type(4)));
-  const int nc = D >> 2;  // <= 256 chunks
-  f32x4 g4[4], b4[4];
+  const int nc = D >> 2;
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) s += (v[j][0] + v[j][1]) + (v[j][2] + v[j][3]);  // v = 0 past the row
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+  const float mean = s / (float)D;
+  float q = 0.f;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const int c = lane + 64 * j;
-    if (c < nc) {
-      g4[j] = ((const f32x4*)gamma)[c];
-      b4[j] = ((const f32x4*)beta)[c];
-    }
-  }
-  float cnt = 0.f, ls = 0.f;
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-    if (lane + 64 * j < nc) {
-      cnt += 4.f;
-      ls += (v[j][0] + v[j][1]) + (v[j][2] + v[j][3]);
-    }
-  float mean = cnt > 0.f ? ls / cnt : 0.f, m2 = 0.f;
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
     if (lane + 64 * j < nc) {
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         const float d = v[j][t] - mean;
-        m2 += d * d;
+        q += d * d;
       }
     }
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    const float nb = __shfl_xor(cnt, off), mb = __shfl_xor(mean, off), m2b = __shfl_xor(m2, off);
-    const float n = cnt + nb;
-    if (n > 0.f) {
-      const float delta = mb - mean;
-      mean += delta * (nb / n);
-      m2 += m2b + delta * delta * (cnt * nb / n);
-    }
-    cnt = n;
   }
-  mean = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, mean)));
-  m2 = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, m2)));
-  const float var = m2 / (float)D;
-  const float rstd = rsqrtf(var + eps);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) q += __shfl_xor(q, off);
+  const float rstd = rsqrtf(q / (float)D + eps);
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int c = lane + 64 * j;
     if (c < nc) {
+      const f32x4 g4 = ((const f32x4*)gamma)[c], b4 = ((const f32x4*)beta)[c];
       f32x4 y;
 #pragma unroll
-      for (int t = 0; t < 4; ++t) y[t] = (v[j][t] - mean) * rstd * g4[j][t] + b4[j][t];
+      for (int t = 0; t < 4; ++t) y[t] = (v[j][t] - mean) * rstd * g4[t] + b4[t];
       if (y32) ((f32x4*)y32)[c] = y;
       if (y16) {
         half4 h;
@@ -1287,7 +1264,7 @@ __global__ __launch_bounds__(256) void attention_mfma64t_kernel(AttentionArgs a)
 // are skipped, and every other block is processed identically whatever the batch's length:
 // a sequence's result does not depend on how its batch is padded, for every L. Work per
 // (sequence, head) grows with its own length only, not with a 64-row pad.
-template <int DH, int PF = 1>  // PF 1: operands two key blocks ahead; 0: at the top of each block (A/B)
+template <int DH, int PF = 0>  // PF 0: a key block's operands at its top; 1: two blocks ahead (A/B)
 __global__ __launch_bounds__(256) void attention_flash16_kernel(AttentionArgs a) {
   constexpr int KS = DH / 32;               // 32-dim k-steps of S^T
   constexpr int DB = DH / 16;               // 16-dim blocks of O^T
@@ -1781,9 +1758,12 @@ int launch_attention(const AttentionArgs& a, int dh, hipStream_t s) {
     const int64_t items = (int64_t)a.B * a.H * ((a.L + 15) / 16);
     MRAG_REQUIRE(items < (1ll << 33), "attention: batch too large");
     const dim3 g4((unsigned)((items + 3) / 4));
-    static const bool no_prefetch = [] {  // MRAG_ATTN_PREFETCH=0: operands loaded per block (A/B timing)
+    // operands of a key block loaded together at its top (24.4 us per ViT layer vs 27.1 for the
+    // round-1 K -> MFMA -> V chain); MRAG_ATTN_PREFETCH=1 loads them two blocks ahead instead,
+    // which measured slower (27.0 us: 112 VGPRs halve the occupancy)
+    static const bool no_prefetch = [] {
       const char* e = getenv("MRAG_ATTN_PREFETCH");
-      return e && atoi(e) == 0;
+      return !(e && atoi(e) == 1);
     }();
     auto kern = dh == 64 ? (no_prefetch ? attention_flash16_kernel<64, 0> : attention_flash16_kernel<64, 1>)
                          : (no_prefetch ? attention_flash16_kernel<32, 0> : attention_flash16_kernel<32, 1>);
