@@ -46,11 +46,28 @@ def search_batch(modality: str, user_id: str, query_vecs: np.ndarray, top_k: int
         return out
 
 
+_BRANCH_POOL = None
+
+
+def _branch_pool():
+    """One worker thread for the image branch of ``retrieve_batch`` (created on first use)."""
+    global _BRANCH_POOL
+    if _BRANCH_POOL is None:
+        from concurrent.futures import ThreadPoolExecutor
+
+        _BRANCH_POOL = ThreadPoolExecutor(max_workers=1, thread_name_prefix="mrag-image-branch")
+    return _BRANCH_POOL
+
+
 def retrieve_batch(user_id: str, queries: Sequence[str], top_k_text: Optional[int] = None,
                    top_k_image: Optional[int] = None, rerank: Optional[bool] = None) -> List[List[Dict[str, Any]]]:
     """Fused text+image results per query, batched end to end = ``retrieve(user_id, q)``
     (app/ml/retrieve.py:103-117) for every q. ``rerank`` defaults to RERANK_ENABLED; the
-    cross-encoder is ``retrieve._get_cross_encoder()`` (False -> no rerank, as retrieve)."""
+    cross-encoder is ``retrieve._get_cross_encoder()`` (False -> no rerank, as retrieve).
+
+    The image branch (CLIP text tower -> image search) runs in a worker thread beside the text
+    branch (MiniLM -> text search): each native call returns to its own thread only, so the two
+    branches' GPU work overlaps (the config-5 bench leg measures the same arrangement)."""
     from app.ml import retrieve as r
     from app.ml.embeddings import _ensure_clip, _ensure_processor, _normalize, _to_numpy
 
@@ -59,13 +76,20 @@ def retrieve_batch(user_id: str, queries: Sequence[str], top_k_text: Optional[in
     qs = list(queries)
     if not qs:
         return []
-    text_vecs = r.embed_text_batch(qs)
-    proc, model = _ensure_processor(), _ensure_clip()
-    img_vecs = _normalize(_to_numpy(model.get_text_features(**proc(text=qs))))
-    blank = np.array([not q.strip() for q in qs])
-    img_vecs[blank] = 0.0
-    th = search_batch("text", user_id, text_vecs, tk)
-    ih = search_batch("image", user_id, img_vecs, ik)
+
+    def image_branch():
+        proc, model = _ensure_processor(), _ensure_clip()
+        img_vecs = _normalize(_to_numpy(model.get_text_features(**proc(text=qs))))
+        blank = np.array([not q.strip() for q in qs])
+        img_vecs[blank] = 0.0
+        return search_batch("image", user_id, img_vecs, ik)
+
+    fut = _branch_pool().submit(image_branch)
+    try:
+        text_vecs = r.embed_text_batch(qs)
+        th = search_batch("text", user_id, text_vecs, tk)
+    finally:
+        ih = fut.result()  # re-raises the image branch's error, after the text branch is done
     _, meta = _store()
     out = []
     for i in range(len(qs)):
