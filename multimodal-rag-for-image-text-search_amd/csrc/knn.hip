@@ -986,11 +986,11 @@ __global__ __launch_bounds__(SCAN2_THREADS) void knn_scan3_kernel(ScanParams p) 
   }
 
   if constexpr (MODE == 1) {
-    // two maxima per (split, query) over disjoint rows: lane groups {0, 1} and {2, 3}
 #pragma unroll
     for (int qb = 0; qb < 4; ++qb) {
-      const float m = fmaxf(smax[qb], __shfl_xor(smax[qb], 16));
-      if ((g4 & 1) == 0) p.part_s[((size_t)split * p.Qp + slot0 + 16 * qb) * 2 + (g4 >> 1)] = m;
+      // four maxima per (split, query) over disjoint rows: lane group g4 = 0..3 (theta_init
+      // takes the k-th largest of all splits' values: a valid lower bound, tighter than two)
+      p.part_s[((size_t)split * p.Qp + slot0 + 16 * qb) * 4 + g4] = smax[qb];
     }
     return;
   }
@@ -1663,15 +1663,15 @@ __global__ __launch_bounds__(SCAN4_THREADS) void knn_scan4_kernel(ScanParams p) 
 // query; k rounds of wave arg-max extraction.
 constexpr float THETA_SEED_MARGIN = (float)(2.5 * EPS_F16);
 __global__ __launch_bounds__(64) void theta_init_kernel(const float* __restrict__ smax, int nvals, int Qp, int k,
-                                                        uint32_t* __restrict__ theta) {
-  constexpr int PER_LANE = 8;  // nvals = 2 * splits <= 512
+                                                        uint32_t* __restrict__ theta, int per) {
+  constexpr int PER_LANE = 16;  // nvals = per * splits <= 4 * 256
   const int q = blockIdx.x, lane = threadIdx.x;
   float v[PER_LANE];
 #pragma unroll
   for (int t = 0; t < PER_LANE; ++t) {
     const int i = lane + 64 * t;
-    // value i = (split i>>1, half i&1)
-    v[t] = i < nvals ? smax[((size_t)(i >> 1) * Qp + q) * 2 + (i & 1)] : -INFINITY;
+    // value i = (split i / per, part i % per); per = 2 (v2 / v4 / v5 pre-pass) or 4 (v3)
+    v[t] = i < nvals ? smax[((size_t)(i / per) * Qp + q) * per + (i % per)] : -INFINITY;
   }
   float kth = -INFINITY;
   for (int r = 0; r < k; ++r) {
@@ -2746,8 +2746,11 @@ int mrag_knn_search(mrag_knn_index* ix, const float* queries, int64_t nq, int32_
       else
         hipLaunchKernelGGL(use_v3 ? get_scan3(DP, true) : get_scan2(DP, true), sgrid, dim3(SCAN2_THREADS), 0, s, sp);
       MRAG_CHECK_LAUNCH();
-      hipLaunchKernelGGL(theta_init_kernel, dim3((unsigned)nq), dim3(64), 0, s, (const float*)sp.part_s, 2 * S,
-                         (int)Qp, k, sp.theta);
+      // sample maxima per (split, query): 4 from the v3 pre-pass (one per lane group; merging them
+      // in pairs, the round-1 seed, measured 0.2 % slower in the main scan), 2 from the others
+      const int per = (use_v3 && !use_v4 && !use_v5) ? 4 : 2;
+      hipLaunchKernelGGL(theta_init_kernel, dim3((unsigned)nq), dim3(64), 0, s, (const float*)sp.part_s, per * S,
+                         (int)Qp, k, sp.theta, per);
       MRAG_CHECK_LAUNCH();
     }
     if (ix->profile) MRAG_HIP(hipEventRecord(ix->ev0, s));
