@@ -54,6 +54,7 @@ struct DeviceGuard {
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 // Monotone float -> uint32 map (ascending float == ascending uint).
 __device__ __forceinline__ uint32_t mrag_f2ord(float f) {

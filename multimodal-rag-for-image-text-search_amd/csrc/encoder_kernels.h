@@ -19,6 +19,10 @@ struct GemmArgs {
   const float* bias;  // [N] or null
   void* C;            // [M][ldc] f16 or f32 per epilogue
   int M, N, K, lda, ldw, ldc;
+  // K3d stream-K workspace (set by the launcher, null otherwise): per workgroup two 256 KiB
+  // partial-accumulator slots, and one arrival counter per output tile (zero between launches)
+  float* sk_part;
+  int* sk_cnt;
 };
 
 struct LayerNormArgs {

@@ -13,6 +13,8 @@
 #include <algorithm>
 #include <type_traits>
 #include <cstdlib>
+#include <map>
+#include <mutex>
 
 #include "common.h"
 #include "encoder_kernels.h"
@@ -310,20 +312,41 @@ __device__ __forceinline__ void vmcnt_wait(int n) {  // n wave-uniform, 0..63
 // ABL (timing experiments only, wrong results): 1 = no LDS-DMA in the loop, 2 = no
 // fragment ds_reads in the loop, 3 = both, 4 = no ping-pong stagger, 5 = LDS-DMA from the
 // first two K-tiles only (L2-hot), 7 = no epilogue stores
-template <int EPI, int ABL = 0, int CFG = 0>
+//
+// SK = 1: stream-K. The tiles of an XCD (the same contiguous range as above) are laid out as
+// one sequence of K-tile iterations (tile-major) and cut into nbx equal contiguous ranges, one
+// per workgroup of that XCD, so every CU gets the same number of MFMA K-steps however the tile
+// count divides by 256 (ViT fc2 / out-proj: 150 tiles; fc1: 600). A range is a list of
+// segments (tile, k-tiles [kb, ke)); even workgroups walk their range forward, odd ones
+// backward, so the two pieces of a tile cut between workgroups s and s + 1 are computed at the
+// same time (both at the start or both at the end of their ranges). A piece of a cut tile
+// stores its raw accumulators to its slot (`sc1` 16-byte stores, each wave drains them, a
+// barrier), one lane adds to the tile's arrival counter (agent-scope atomic), and the
+// workgroup whose add comes last sums every piece IN K ORDER (p0 + p1 (+ p2), own piece from
+// registers, the others by `sc1` loads), resets the counter and runs the normal epilogue:
+// no workgroup ever waits for another (MI355X_MICROARCH.md, hand-off table row 1). The sum
+// order depends only on the cut points, i.e. on (M, N, K, grid): a launch is deterministic,
+// but a row's last bits can differ between batch sizes that cut differently (the launcher
+// uses SK only from M >= 8192 rows, so smaller batches keep the one-accumulator order).
+constexpr int SK_SLOT_BYTES = 256 * 256 * 4;  // one CFG-0 tile of f32 accumulators
+
+template <int EPI, int ABL = 0, int CFG = 0, int SK = 0>
 __global__ __launch_bounds__(G8_THREADS) void gemm_8p_kernel(GemmArgs g) {
   using GG = G8Geom<CFG>;
   constexpr int BM = GG::BM, BN = GG::BN, WM = GG::WM, WN = GG::WN, HM = GG::HM, HN = GG::HN;
   constexpr int NI = GG::NI, NJ = GG::NJ, PA = GG::PA, PB = GG::PB;
-  __shared__ __attribute__((aligned(16))) char smem[2 * G8_BUF + (ABL == 8 ? 16 : G8_BIAS_MAX * 4)];
+  static_assert(SK == 0 || (CFG == 0 && ABL == 0), "stream-K: 256 x 256 tiles only");
+  constexpr int BIAS_BYTES = ABL == 8 ? 16 : G8_BIAS_MAX * 4;
+  __shared__ __attribute__((aligned(16))) char smem[2 * G8_BUF + BIAS_BYTES + 16];
   float* sbias = (float*)(smem + 2 * G8_BUF);
+  int* sflag = (int*)(smem + 2 * G8_BUF + BIAS_BYTES);
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wr = w >> 2, wc = w & 3;
   const int fr = lane & 15, fq = lane >> 4;
   const uint32_t lds_base = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)((AS3 char*)smem));
 
-  // this workgroup's tiles: lo + s + k * nbx, k = 0 .. my_n - 1
+  // this workgroup's tiles: lo + s + k * nbx, k = 0 .. my_n - 1 (SK: see above)
   const int tiles_n = g.N / BN;
   const int ntiles = ((g.M + BM - 1) / BM) * tiles_n;
   const int xcd = blockIdx.x & 7, sidx = blockIdx.x >> 3;
@@ -332,16 +355,36 @@ __global__ __launch_bounds__(G8_THREADS) void gemm_8p_kernel(GemmArgs g) {
   const int lo = xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8;
   const int cnt = q8 + (xcd < r8 ? 1 : 0);
   const int my_n = sidx < cnt ? (cnt - sidx + nbx - 1) / nbx : 0;
-  if (my_n == 0) return;  // whole workgroup, before any barrier
+  const int ktiles = g.K / GK;
+  const int64_t Ix = (int64_t)cnt * ktiles;  // SK: K-tile iterations of this XCD
+  auto range_lo = [&](int s) { return (int64_t)s * Ix / nbx; };
+  const int64_t it0 = SK ? range_lo(sidx) : 0, it1 = SK ? range_lo(sidx + 1) : 0;
+  const int t_first = SK ? (int)(it0 / ktiles) : 0, t_last = SK ? (int)((it1 - 1) / ktiles) : 0;
+  const bool fwd = (sidx & 1) == 0;
+  const int nseg = SK ? (it1 > it0 ? t_last - t_first + 1 : 0) : my_n;
+  if (nseg == 0) return;  // whole workgroup, before any barrier
+  // segment i of this workgroup: tile T, k-tiles [kb, ke)
+  auto seg = [&](int i, int& T, int& kb, int& ke) {
+    if constexpr (SK) {
+      const int t = fwd ? t_first + i : t_last - i;
+      const int64_t base = (int64_t)t * ktiles;
+      kb = (int)(it0 > base ? it0 - base : 0);
+      ke = (int)(it1 - base < ktiles ? it1 - base : ktiles);
+      T = lo + t;
+    } else {
+      T = lo + sidx + i * nbx;
+      kb = 0;
+      ke = ktiles;
+    }
+  };
 
   if constexpr (ABL != 8) {
     for (int i = threadIdx.x; i < g.N; i += G8_THREADS) sbias[i] = g.bias ? g.bias[i] : 0.f;
     __syncthreads();
   }
 
-  const int ktiles = g.K / GK;
-  const int KH = 4 * ktiles;       // half-tiles per tile
-  const int total = my_n * KH;     // half-tiles of the whole stream
+  const int KH = 4 * ktiles;                                // half-tiles per tile
+  const int total = SK ? (int)(4 * (it1 - it0)) : my_n * KH;  // half-tiles of the whole stream
 
   // staging: a slot with PX pieces per wave gets pieces PX w .. PX w + PX - 1 (8 LDS rows each)
   // from this wave; LDS row j = 8 (PX w + q) + (lane >> 3), chunk position lane & 7 holds
@@ -367,7 +410,8 @@ __global__ __launch_bounds__(G8_THREADS) void gemm_8p_kernel(GemmArgs g) {
   // a K-tile always issues slot (p + 3) & 3, a compile-time constant, so the loader keeps
   // its K-tile position incrementally and recomputes this lane's source-row element
   // offsets once per tile (no per-phase division or slot selection).
-  int ld_kt = 0, ld_par = 0, ld_T = lo + sidx;
+  int ld_kt, ld_ke, ld_T, ld_seg = 0, ld_par = 0;
+  seg(0, ld_T, ld_kt, ld_ke);
   int gA[2][PA], gB[2][PB];  // element offsets (row * ld + chunk) for the tile being loaded
   auto load_tile_offsets = [&]() {
     const int tm = ld_T / tiles_n;
@@ -397,9 +441,8 @@ __global__ __launch_bounds__(G8_THREADS) void gemm_8p_kernel(GemmArgs g) {
     }
     if constexpr (sl == 3) {  // K-tile complete: advance the loader
       ld_par ^= 1;
-      if (++ld_kt == ktiles) {
-        ld_kt = 0;
-        ld_T += nbx;
+      if (++ld_kt == ld_ke && ++ld_seg < nseg) {
+        seg(ld_seg, ld_T, ld_kt, ld_ke);
         load_tile_offsets();
       }
     }
@@ -494,10 +537,87 @@ __global__ __launch_bounds__(G8_THREADS) void gemm_8p_kernel(GemmArgs g) {
     vmcnt_wait(younger(1, last));  // L[0], L[1] landed
     bar();
   }
+  // SK: the piece of local tile t held in `acc` (tile id T) is stored; returns true when this
+  // workgroup's piece arrived last and `acc` now holds the whole tile's sum (see above)
+  auto sk_piece = [&](int t, int T) -> bool {
+    if (wr == 0) bar();  // group 0 waits for group 1's last phase: both groups aligned
+    const __amdgpu_buffer_rsrc_t part = __builtin_amdgcn_make_buffer_rsrc(g.sk_part, 0, 0x7fffffff, 0x00020000);
+    const uint32_t tid16 = threadIdx.x * 16;
+    {
+      const uint32_t base = (uint32_t)(2 * blockIdx.x + (t == t_first ? 0 : 1)) * SK_SLOT_BYTES + tid16;
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+          for (int i = 0; i < NI; ++i)
+#pragma unroll
+            for (int jb = 0; jb < NJ; ++jb) {
+              const int r = ((h * 2 + hh) * NI + i) * NJ + jb;
+              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[h][hh][i][jb]), part,
+                                                     base + r * (G8_THREADS * 16), 0, 16 /* sc1 */);
+            }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's piece has left the CU
+    bar();
+    if (threadIdx.x == 0)
+      *sflag = __hip_atomic_fetch_add(g.sk_cnt + T, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const int arrived = *sflag;
+    // the pieces of tile t: workgroups s_first .. s_last of this XCD, ascending s = ascending k
+    const int64_t tb = (int64_t)t * ktiles;
+    const int s_first = (int)(((tb + 1) * nbx - 1) / Ix), s_last = (int)(((tb + ktiles) * nbx - 1) / Ix);
+    int np = 0;
+    for (int s = s_first; s <= s_last; ++s) np += range_lo(s + 1) > range_lo(s) ? 1 : 0;
+    if (arrived != np - 1) return false;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        f32x4 v[NI][NJ];
+        bool first = true;
+        for (int s = s_first; s <= s_last; ++s) {
+          const int64_t a0 = range_lo(s), a1 = range_lo(s + 1);
+          if (a1 <= a0) continue;
+          if (s == sidx) {
+#pragma unroll
+            for (int i = 0; i < NI; ++i)
+#pragma unroll
+              for (int jb = 0; jb < NJ; ++jb) v[i][jb] = first ? acc[h][hh][i][jb] : v[i][jb] + acc[h][hh][i][jb];
+          } else {
+            const uint32_t base =
+                (uint32_t)(2 * (xcd + 8 * s) + (t == (int)(a0 / ktiles) ? 0 : 1)) * SK_SLOT_BYTES + tid16;
+            f32x4 p[NI][NJ];
+#pragma unroll
+            for (int i = 0; i < NI; ++i)
+#pragma unroll
+              for (int jb = 0; jb < NJ; ++jb) {
+                const int r = ((h * 2 + hh) * NI + i) * NJ + jb;
+                p[i][jb] = __builtin_bit_cast(
+                    f32x4, __builtin_amdgcn_raw_buffer_load_b128(part, base + r * (G8_THREADS * 16), 0, 16 /* sc1 */));
+              }
+#pragma unroll
+            for (int i = 0; i < NI; ++i)
+#pragma unroll
+              for (int jb = 0; jb < NJ; ++jb) v[i][jb] = first ? p[i][jb] : v[i][jb] + p[i][jb];
+          }
+          first = false;
+        }
+#pragma unroll
+        for (int i = 0; i < NI; ++i)
+#pragma unroll
+          for (int jb = 0; jb < NJ; ++jb) acc[h][hh][i][jb] = v[i][jb];
+      }
+    if (threadIdx.x == 0) __hip_atomic_store(g.sk_cnt + T, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return true;
+  };
+
   // waves 4..7 (one per SIMD beside a wave of 0..3) run one barrier behind waves 0..3
   if (ABL != 4 && wr == 1) bar();
   int phi = 0;
-  for (int tl = 0; tl < my_n; ++tl) {
+  for (int sg = 0; sg < nseg; ++sg) {
+    int T, kb, ke;
+    seg(sg, T, kb, ke);
 #pragma unroll
     for (int h = 0; h < 2; ++h)
 #pragma unroll
@@ -506,7 +626,7 @@ __global__ __launch_bounds__(G8_THREADS) void gemm_8p_kernel(GemmArgs g) {
         for (int i = 0; i < NI; ++i)
 #pragma unroll
           for (int jb = 0; jb < NJ; ++jb) acc[h][hh][i][jb] = f32x4{};
-    for (int kt = 0; kt < ktiles; ++kt, phi += 4) {
+    for (int kt = kb; kt < ke; ++kt, phi += 4) {
       const char* buf = (const char*)smem + ((phi >> 2) & 1) * G8_BUF;
       readA(buf + GG::slot_off(0));  // phase 0: (h0, hh0)
       readB(buf + GG::slot_off(1), fb0);
@@ -527,11 +647,15 @@ __global__ __launch_bounds__(G8_THREADS) void gemm_8p_kernel(GemmArgs g) {
     }
     st_phi = phi - 1;
     st_cnt = 0;
+    const bool split = SK && (kb != 0 || ke != ktiles);  // wave-uniform
+    if (split && !sk_piece(T - lo, T)) {
+      if (wr == 1) bar();  // restore the stagger (the workgroup's barrier counts stay equal)
+      continue;
+    }
 
     // epilogue: blocks (h, hh, i): row WM wr + HM h + 16 i + fr; columns WN wc + HN hh + 8 fq
     // + (0..7) from the block pair jb = 0, 1 (one 16-byte f16 store, two for f32) and, for
     // CFG 1, WN wc + HN hh + 32 + 4 fq + (0..3) from jb = 2 (one 8-byte f16 / 16-byte f32 store)
-    const int T = lo + sidx + tl * nbx;
     const int tm = T / tiles_n;
     const int m0 = tm * BM, n0 = (T - tm * tiles_n) * BN;
     constexpr int SPB = ((EPI == EPI_F32_RESIDUAL || EPI == EPI_F32) ? 2 : 1) + (NJ == 3 ? 1 : 0);
@@ -564,6 +688,7 @@ __global__ __launch_bounds__(G8_THREADS) void gemm_8p_kernel(GemmArgs g) {
         }
       }
     }
+    if (split && wr == 1) bar();  // restore the stagger after a cut tile's epilogue
   }
   if (ABL != 4 && wr == 0) bar();  // same barrier count for both groups
 }
@@ -1588,10 +1713,106 @@ bool k3_beats_k3d(const GemmArgs& g) {
   return 2 * r_3 < 3 * r_d;  // K3 time ~ (2/3) r_3 < r_d; ties stay on K3d
 }
 
+// K3d stream-K (SK) policy: env MRAG_G8_SK = 0 (default) off, 1 where the estimate says it
+// beats the data-parallel tile rounds, 2 wherever K3d runs (tests, A/B). Estimated in K-tile
+// steps per CU: DP = ceil(tiles / CUs) * k-tiles; SK = tiles * k-tiles / CUs, +15 % and +2
+// steps for the cut tiles' partial hand-off. Batches under 8192 rows keep the data-parallel
+// order (a row computed alone and inside such a batch is bit-identical). Measured SLOWER on
+// every ViT shape (fc2 106 -> 127 us, out-proj 46 -> 78, fc1 88 -> 109; CLIP 60.7k -> 46.8k
+// img/s, one box): a cut 256 x 256 tile hands off 256 KiB of f32 partials each way, ~110 MB
+// per out-proj launch against its 118 MB of operand fills (notes/gemm_experiments.md).
+int g8_sk_mode() {
+  static const int v = [] {
+    const char* e = getenv("MRAG_G8_SK");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
+bool g8_use_sk(const GemmArgs& g, int ntiles, int cus) {
+  const int mode = g8_sk_mode();
+  if (mode <= 0) return false;
+  if (mode >= 2) return true;
+  if (g.M < 8192) return false;
+  const double kt = g.K / GK;
+  const double dp = (double)((ntiles + cus - 1) / cus) * kt;
+  const double sk = 1.15 * ntiles * kt / cus + 2.0;
+  return sk < dp;
+}
+
+// Per-(device, stream) SK workspace: 2 partial slots per workgroup (grid <= CUs) and one
+// arrival counter per tile, zeroed once (every launch leaves them zero). Launches on one
+// stream are ordered, so they can share it; concurrent streams get their own.
+struct SkWorkspace {
+  float* part = nullptr;
+  int* cnt = nullptr;
+  int slots = 0, counters = 0;
+};
+
+int sk_workspace(hipStream_t s, int grid, int ntiles, GemmArgs& g) {
+  static std::mutex mu;
+  static std::map<std::pair<int, hipStream_t>, SkWorkspace> pool;
+  int dev = 0;
+  MRAG_HIP(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> lk(mu);
+  SkWorkspace& w = pool[{dev, s}];
+  if (w.slots < 2 * grid) {
+    if (w.part) {
+      MRAG_HIP(hipStreamSynchronize(s));
+      MRAG_HIP(hipFree(w.part));
+      w.part = nullptr;
+      w.slots = 0;
+    }
+    MRAG_HIP(hipMalloc(&w.part, (size_t)2 * grid * SK_SLOT_BYTES));
+    w.slots = 2 * grid;
+  }
+  if (w.counters < ntiles) {
+    if (w.cnt) {
+      MRAG_HIP(hipStreamSynchronize(s));
+      MRAG_HIP(hipFree(w.cnt));
+      w.cnt = nullptr;
+      w.counters = 0;
+    }
+    const int n = std::max(ntiles, 4096);
+    MRAG_HIP(hipMalloc(&w.cnt, (size_t)n * 4));
+    MRAG_HIP(hipMemsetAsync(w.cnt, 0, (size_t)n * 4, s));
+    w.counters = n;
+  }
+  g.sk_part = w.part;
+  g.sk_cnt = w.cnt;
+  return MRAG_OK;
+}
+
+template <int EPI>
+int launch_gemm_8p_sk(const GemmArgs& g0, hipStream_t s) {
+  const int ntiles = ((g0.M + 255) / 256) * (g0.N / 256);
+  const int nb = std::max(8, num_cus() / 8 * 8);
+  GemmArgs g = g0;
+  if (int rc = sk_workspace(s, nb, ntiles, g)) return rc;
+  static bool said = false;
+  if (!said && getenv("MRAG_G8_VERBOSE")) {
+    fprintf(stderr, "K3d stream-K: %d CUs, grid %d for %d tiles x %d k-tiles\n", num_cus(), nb, ntiles, g.K / GK);
+    said = true;
+  }
+  hipLaunchKernelGGL((gemm_8p_kernel<EPI, 0, 0, 1>), dim3((unsigned)nb), dim3(G8_THREADS), 0, s, g);
+  MRAG_CHECK_LAUNCH();
+  return MRAG_OK;
+}
+
 template <int CFG>
 int launch_gemm_8p_cfg(const GemmArgs& g, int epi, hipStream_t s) {
   using GG = G8Geom<CFG>;
   const int ntiles = ((g.M + GG::BM - 1) / GG::BM) * (g.N / GG::BN);
+  if (CFG == 0 && g8_use_sk(g, ntiles, std::max(8, num_cus() / 8 * 8))) {
+    switch (epi) {
+      case EPI_F16: return launch_gemm_8p_sk<EPI_F16>(g, s);
+      case EPI_F16_QUICK_GELU: return launch_gemm_8p_sk<EPI_F16_QUICK_GELU>(g, s);
+      case EPI_F16_GELU_ERF: return launch_gemm_8p_sk<EPI_F16_GELU_ERF>(g, s);
+      case EPI_F32_RESIDUAL: return launch_gemm_8p_sk<EPI_F32_RESIDUAL>(g, s);
+      case EPI_F32: return launch_gemm_8p_sk<EPI_F32>(g, s);
+      default: return mrag::fail(MRAG_ERR_ARG, "gemm: bad epilogue %d", epi);
+    }
+  }
   int nb = std::min((ntiles + 7) / 8 * 8, std::max(8, num_cus() / 8 * 8));
   static const int grid_override = [] {
     const char* e = getenv("MRAG_G8_GRID");
