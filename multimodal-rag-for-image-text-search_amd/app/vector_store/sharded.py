@@ -49,9 +49,28 @@ class ShardedFlatIndex:
 
     def search(self, queries, k: int, label: int = -1) -> Tuple:
         """(scores f32 [nq,k], rows int64 [nq,k]) over the whole sharded corpus."""
+        return self.combine(self.search_local(queries, k, label=label), k)
+
+    def search_local(self, queries, k: int, label: int = -1) -> Tuple:
+        """Step 1 alone: this shard's exact top-k with global row ids (plus the f64 scores the
+        merge orders by when world > 1). Safe to run from several host threads at once, each on
+        its own stream (the library gives every search its own workspace)."""
         if self.world == 1:
             return self.local.search(queries, k, label=label, row_offset=self.row_offset)
-        s, r, s64 = self.local.search(queries, k, label=label, row_offset=self.row_offset, with_f64=True)
+        return self.local.search(queries, k, label=label, row_offset=self.row_offset, with_f64=True)
+
+    def combine(self, local, k: int) -> Tuple:
+        """Steps 2-3 on the calling thread's current stream: all-gather + K11 merge. Every rank
+        must combine its searches in the same order (one communicator)."""
+        if self.world == 1:
+            return local
+        import torch
+
+        s, r, s64 = local
+        if s64.is_cuda:  # produced on another stream: keep the memory until this one is done
+            cur = torch.cuda.current_stream(s64.device)
+            for t in (s64, r):
+                t.record_stream(cur)
         ms, mr, _ = self._merge(self._gather(s64), self._gather(r), k)
         return ms, mr
 

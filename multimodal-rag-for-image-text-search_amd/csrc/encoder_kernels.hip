@@ -967,8 +967,19 @@ __global__ __launch_bounds__(256) void layernorm_kernel(LayerNormArgs a) {
 // stores); two-pass mean / variance in f32 from registers: one HBM pass over the row. (A
 // single butterfly merging per-lane (count, mean, M2) pairs measured slower: 16.2 vs 12.5 us
 // per ViT LayerNorm — three shuffles and a division per round.)
-__device__ __forceinline__ void ln_row4(f32x4 (&v)[4], int lane, int D, float eps, const float* gamma,
-                                        const float* beta, float* y32, _Float16* y16) {
+// gamma / beta chunks of this lane, loaded before the row's reductions (off their latency path)
+__device__ __forceinline__ void ln_params4(int lane, int D, const float* gamma, const float* beta, f32x4 (&g4)[4],
+                                           f32x4 (&b4)[4]) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int c = lane + 64 * j;
+    g4[j] = c < (D >> 2) ? ((const f32x4*)gamma)[c] : f32x4{};
+    b4[j] = c < (D >> 2) ? ((const f32x4*)beta)[c] : f32x4{};
+  }
+}
+
+__device__ __forceinline__ void ln_row4p(f32x4 (&v)[4], int lane, int D, float eps, const f32x4 (&g4)[4],
+                                         const f32x4 (&b4)[4], float* y32, _Float16* y16) {
   typedef _Float16 half4 __attribute__((ext_vector_type(4)));
   const int nc = D >> 2;
   float s = 0.f;
@@ -995,10 +1006,9 @@ __device__ __forceinline__ void ln_row4(f32x4 (&v)[4], int lane, int D, float ep
   for (int j = 0; j < 4; ++j) {
     const int c = lane + 64 * j;
     if (c < nc) {
-      const f32x4 g4 = ((const f32x4*)gamma)[c], b4 = ((const f32x4*)beta)[c];
       f32x4 y;
 #pragma unroll
-      for (int t = 0; t < 4; ++t) y[t] = (v[j][t] - mean) * rstd * g4[t] + b4[t];
+      for (int t = 0; t < 4; ++t) y[t] = (v[j][t] - mean) * rstd * g4[j][t] + b4[j][t];
       if (y32) ((f32x4*)y32)[c] = y;
       if (y16) {
         half4 h;
@@ -1010,17 +1020,40 @@ __device__ __forceinline__ void ln_row4(f32x4 (&v)[4], int lane, int D, float ep
   }
 }
 
+__device__ __forceinline__ void ln_row4(f32x4 (&v)[4], int lane, int D, float eps, const float* gamma,
+                                        const float* beta, float* y32, _Float16* y16) {
+  f32x4 g4[4], b4[4];
+  ln_params4(lane, D, gamma, beta, g4, b4);
+  ln_row4p(v, lane, D, eps, g4, b4, y32, y16);
+}
+
+// RPW rows per wave (consecutive): every row's loads and the gamma / beta chunks are issued
+// before the first reduction, so a wave keeps RPW rows of loads in flight and a ViT / config-5
+// LayerNorm fits the chip in one round of workgroups (RPW = 2: 12,800 rows -> 1,600
+// workgroups) instead of 1.6 rounds with a tail. Per-row arithmetic is unchanged.
+template <int RPW>
 __global__ __launch_bounds__(256) void layernorm4_kernel(LayerNormArgs a) {
   const int lane = threadIdx.x & 63;
-  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (r >= a.rows) return;
-  const int src = a.gather ? a.gather[r] : r;
-  const f32x4* x = (const f32x4*)(a.x + (size_t)src * a.ldx);
-  f32x4 v[4];
+  const int r0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW;
+  if (r0 >= a.rows) return;
+  f32x4 v[RPW][4];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) v[j] = lane + 64 * j < (a.D >> 2) ? x[lane + 64 * j] : f32x4{};
-  ln_row4(v, lane, a.D, a.eps, a.gamma, a.beta, a.y32 ? a.y32 + (size_t)r * a.D : nullptr,
-          a.y16 ? a.y16 + (size_t)r * a.D : nullptr);
+  for (int rr = 0; rr < RPW; ++rr) {
+    const int r = r0 + rr < a.rows ? r0 + rr : r0;
+    const int src = a.gather ? a.gather[r] : r;
+    const f32x4* x = (const f32x4*)(a.x + (size_t)src * a.ldx);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[rr][j] = lane + 64 * j < (a.D >> 2) ? x[lane + 64 * j] : f32x4{};
+  }
+  f32x4 g4[4], b4[4];
+  ln_params4(lane, a.D, a.gamma, a.beta, g4, b4);
+#pragma unroll
+  for (int rr = 0; rr < RPW; ++rr) {
+    const int r = r0 + rr;
+    if (r < a.rows)
+      ln_row4p(v[rr], lane, a.D, a.eps, g4, b4, a.y32 ? a.y32 + (size_t)r * a.D : nullptr,
+               a.y16 ? a.y16 + (size_t)r * a.D : nullptr);
+  }
 }
 
 // ViT token assembly + pre_layrnorm in one pass (modeling_clip.py:212-217, :642):
@@ -1916,8 +1949,14 @@ int launch_layernorm(const LayerNormArgs& a, hipStream_t s) {
   MRAG_REQUIRE(a.D > 0 && a.D <= 1024, "layernorm: D=%d unsupported", a.D);
   const bool vec4 = a.D % 4 == 0 && a.ldx % 4 == 0 && ((uintptr_t)a.x & 15) == 0 && ((uintptr_t)a.gamma & 15) == 0 &&
                     ((uintptr_t)a.beta & 15) == 0 && ((uintptr_t)a.y32 & 15) == 0 && ((uintptr_t)a.y16 & 7) == 0;
-  if (vec4)
-    hipLaunchKernelGGL(layernorm4_kernel, dim3((unsigned)((a.rows + 3) / 4)), dim3(256), 0, s, a);
+  static const int rpw = [] {  // env MRAG_LN_RPW = 2: two rows per wave (measured slower: 14.3 vs 12.3 us)
+    const char* e = getenv("MRAG_LN_RPW");
+    return e && atoi(e) == 2 ? 2 : 1;
+  }();
+  if (vec4 && rpw == 2)
+    hipLaunchKernelGGL(layernorm4_kernel<2>, dim3((unsigned)((a.rows + 7) / 8)), dim3(256), 0, s, a);
+  else if (vec4)
+    hipLaunchKernelGGL(layernorm4_kernel<1>, dim3((unsigned)((a.rows + 3) / 4)), dim3(256), 0, s, a);
   else
     hipLaunchKernelGGL(layernorm_kernel, dim3((unsigned)((a.rows + 3) / 4)), dim3(256), 0, s, a);
   MRAG_CHECK_LAUNCH();

@@ -28,6 +28,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <mutex>
+#include <shared_mutex>
 #include <type_traits>
 #include <utility>
 #include <vector>
@@ -2341,29 +2342,40 @@ int64_t next_pow2(int64_t x) {
 
 }  // namespace
 
+// Per-search buffers. A search takes a free context from its index's pool (a new one when all
+// are in use), so several host threads can search one index at once, each on its own stream,
+// while the corpus buffers stay shared and read-only (adds / deletes take the index lock
+// exclusively). Two searches in flight let one search's K8 / certificate / host round trip run
+// beside the other's scan (bench.py runs the kNN leg that way on one GPU).
+struct SearchCtx {
+  DevBuf qin, q32, qn, q16, part_s, part_i, thresh, fail_list, counters, cand_cnt, cand, scratch;
+  DevBuf out_s, out_s64, out_r, theta, part_tau;
+  int32_t* host_counters = nullptr;  // pinned [2]: fail_cnt, overflow
+  hipEvent_t done = nullptr;         // end of the search's device work (waited by spinning)
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;  // scan timing (mrag_knn_profile)
+  mrag_knn::Workspace gws[8];               // K7g buffers
+};
+
 struct mrag_knn_index {
-  std::mutex mu;
+  std::mutex mu;             // serialises mutations (add / set_labels / destroy) and profile toggles
+  std::shared_mutex rw;      // searches shared, mutations exclusive
   int device = 0;
   int D = 0, DP = 0;
   int64_t n = 0, cap = 0;
   DevBuf x16, x32, xn, labels;
   hipStream_t stream = nullptr;
-  // search workspace
-  DevBuf qin, q32, qn, q16, part_s, part_i, thresh, fail_list, counters, cand_cnt, cand, scratch;
-  DevBuf out_s, out_s64, out_r, stage_rows, stage_labels, rowlist, theta, part_tau;
+  DevBuf stage_rows, stage_labels, rowlist;  // mutation staging
+  std::mutex pool_mu;                        // guards the context pool and the stats below
+  std::vector<SearchCtx*> ctx_all, ctx_free;
   int ablate = 0;  // diagnostic knob, env MRAG_SCAN_ABLATE (timing experiments only)
   bool scan_v1 = false;  // env MRAG_SCAN_V1=1: force the v1 top-k scan (A/B timing)
   bool no_sample = false;  // env MRAG_SCAN_NO_SAMPLE=1: skip the threshold pre-pass (A/B timing)
   bool scan_v2 = false;    // env MRAG_SCAN_V2=1: the 32x32x16 v2 scan instead of v3 (A/B timing)
   bool scan_v4 = false;    // env MRAG_SCAN_V4=1: the two-waves-per-SIMD v4 scan instead of v3 (A/B timing)
   bool scan_v5 = false;    // env MRAG_SCAN_V5=1: the three-buffer 48-row v5 scan instead of v3
-  int32_t* host_counters = nullptr;  // pinned [2]: fail_cnt, overflow
-  hipEvent_t done = nullptr;         // end of a search's device work (waited by spinning)
-  mrag_knn::Workspace gws[8];  // K7g buffers
   int64_t last_uncertified = 0, last_retries = 0;
   // optional scan timing (mrag_knn_profile)
   bool profile = false;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
   double scan_ms = 0.0;
   int64_t scan_launches = 0;
 };
@@ -2375,14 +2387,61 @@ namespace {
 // only once its device work is done; polling wakes the host within a microsecond or two of the
 // last kernel, where a stream synchronize could leave the GPU idle for tens of microseconds
 // between back-to-back searches.
-int wait_stream(mrag_knn_index* ix, hipStream_t s) {
-  MRAG_HIP(hipEventRecord(ix->done, s));
+int wait_stream(SearchCtx* c, hipStream_t s) {
+  MRAG_HIP(hipEventRecord(c->done, s));
   hipError_t e;
-  while ((e = hipEventQuery(ix->done)) == hipErrorNotReady) {
+  while ((e = hipEventQuery(c->done)) == hipErrorNotReady) {
   }
   if (e != hipSuccess) return mrag::fail(MRAG_ERR_HIP, "search: %s", hipGetErrorString(e));
   return MRAG_OK;
 }
+
+void ctx_free_all(SearchCtx* c) {
+  for (DevBuf* b : {&c->qin, &c->q32, &c->qn, &c->q16, &c->part_s, &c->part_i, &c->thresh, &c->fail_list,
+                    &c->counters, &c->cand_cnt, &c->cand, &c->scratch, &c->out_s, &c->out_s64, &c->out_r,
+                    &c->theta, &c->part_tau})
+    release(*b);
+  mrag_knn::release(c->gws);
+  if (c->host_counters) (void)hipHostFree(c->host_counters);
+  if (c->done) (void)hipEventDestroy(c->done);
+  if (c->ev0) (void)hipEventDestroy(c->ev0);
+  if (c->ev1) (void)hipEventDestroy(c->ev1);
+  delete c;
+}
+
+// A free search context of ix (created on first need); returned by ctx_put.
+int ctx_get(mrag_knn_index* ix, SearchCtx** out) {
+  {
+    std::lock_guard<std::mutex> lk(ix->pool_mu);
+    if (!ix->ctx_free.empty()) {
+      *out = ix->ctx_free.back();
+      ix->ctx_free.pop_back();
+      return MRAG_OK;
+    }
+  }
+  auto* c = new SearchCtx();
+  hipError_t e = hipHostMalloc((void**)&c->host_counters, 16, hipHostMallocDefault);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->done, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreate(&c->ev0);
+  if (e == hipSuccess) e = hipEventCreate(&c->ev1);
+  if (e != hipSuccess) {
+    ctx_free_all(c);
+    return mrag::fail(MRAG_ERR_HIP, "search context: %s", hipGetErrorString(e));
+  }
+  std::lock_guard<std::mutex> lk(ix->pool_mu);
+  ix->ctx_all.push_back(c);
+  *out = c;
+  return MRAG_OK;
+}
+
+struct CtxLease {
+  mrag_knn_index* ix;
+  SearchCtx* c;
+  ~CtxLease() {
+    std::lock_guard<std::mutex> lk(ix->pool_mu);
+    ix->ctx_free.push_back(c);
+  }
+};
 
 int grow(mrag_knn_index* ix, int64_t need) {
   if (need <= ix->cap) return MRAG_OK;
@@ -2443,8 +2502,6 @@ int mrag_knn_create(int32_t dim, int32_t device, mrag_knn_index** out) {
   if (const char* v4 = getenv("MRAG_SCAN_V4")) ix->scan_v4 = atoi(v4) != 0;
   if (const char* v5 = getenv("MRAG_SCAN_V5")) ix->scan_v5 = atoi(v5) != 0;
   hipError_t e = hipStreamCreateWithFlags(&ix->stream, hipStreamNonBlocking);
-  if (e == hipSuccess) e = hipHostMalloc((void**)&ix->host_counters, 16, hipHostMallocDefault);
-  if (e == hipSuccess) e = hipEventCreateWithFlags(&ix->done, hipEventDisableTiming);
   if (e != hipSuccess) {
     delete ix;
     return mrag::fail(MRAG_ERR_HIP, "stream/pinned alloc: %s", hipGetErrorString(e));
@@ -2458,16 +2515,12 @@ int mrag_knn_destroy(mrag_knn_index* ix) {
   {
     mrag::DeviceGuard g(ix->device);
     (void)hipStreamSynchronize(ix->stream);
-    for (DevBuf* b : {&ix->x16, &ix->x32, &ix->xn, &ix->labels, &ix->qin, &ix->q32, &ix->qn, &ix->q16,
-                      &ix->part_s, &ix->part_i, &ix->thresh, &ix->fail_list, &ix->counters,
-                      &ix->cand_cnt, &ix->cand, &ix->scratch, &ix->out_s, &ix->out_s64, &ix->out_r,
-                      &ix->stage_rows, &ix->stage_labels, &ix->rowlist, &ix->theta, &ix->part_tau})
+    std::unique_lock<std::shared_mutex> wl(ix->rw);  // no search in flight
+    for (DevBuf* b : {&ix->x16, &ix->x32, &ix->xn, &ix->labels, &ix->stage_rows, &ix->stage_labels, &ix->rowlist})
       release(*b);
-    mrag_knn::release(ix->gws);
-    if (ix->host_counters) (void)hipHostFree(ix->host_counters);
-    if (ix->done) (void)hipEventDestroy(ix->done);
-    if (ix->ev0) (void)hipEventDestroy(ix->ev0);
-    if (ix->ev1) (void)hipEventDestroy(ix->ev1);
+    for (SearchCtx* c : ix->ctx_all) ctx_free_all(c);
+    ix->ctx_all.clear();
+    ix->ctx_free.clear();
     if (ix->stream) (void)hipStreamDestroy(ix->stream);
   }
   delete ix;
@@ -2482,6 +2535,7 @@ int mrag_knn_size(const mrag_knn_index* ix, int64_t* n) {
 
 int mrag_knn_last_stats(const mrag_knn_index* ix, int64_t* uncertified, int64_t* retries) {
   MRAG_REQUIRE(ix != nullptr, "NULL index");
+  std::lock_guard<std::mutex> lk(const_cast<mrag_knn_index*>(ix)->pool_mu);
   if (uncertified) *uncertified = ix->last_uncertified;
   if (retries) *retries = ix->last_retries;
   return MRAG_OK;
@@ -2489,11 +2543,8 @@ int mrag_knn_last_stats(const mrag_knn_index* ix, int64_t* uncertified, int64_t*
 
 int mrag_knn_profile(mrag_knn_index* ix, int32_t enable, double* scan_ms_total, int64_t* scan_launches) {
   MRAG_REQUIRE(ix != nullptr, "NULL index");
-  std::lock_guard<std::mutex> lk(ix->mu);
-  mrag::DeviceGuard g(ix->device);
+  std::lock_guard<std::mutex> lk(ix->pool_mu);
   if (enable == 1) {
-    if (!ix->ev0) MRAG_HIP(hipEventCreate(&ix->ev0));
-    if (!ix->ev1) MRAG_HIP(hipEventCreate(&ix->ev1));
     ix->profile = true;
     ix->scan_ms = 0.0;
     ix->scan_launches = 0;
@@ -2511,6 +2562,7 @@ int mrag_knn_add(mrag_knn_index* ix, const float* rows, const int32_t* labels, i
   MRAG_REQUIRE(nrows >= 0, "negative row count");
   MRAG_REQUIRE(ptr_kind == MRAG_PTR_HOST || ptr_kind == MRAG_PTR_DEVICE, "bad ptr_kind %d", ptr_kind);
   std::lock_guard<std::mutex> lk(ix->mu);
+  std::unique_lock<std::shared_mutex> wl(ix->rw);
   mrag::DeviceGuard g(ix->device);
   if (first_row) *first_row = ix->n;
   if (nrows == 0) return MRAG_OK;
@@ -2543,6 +2595,7 @@ int mrag_knn_set_labels(mrag_knn_index* ix, const int64_t* rows, int64_t n, int3
   MRAG_REQUIRE(n >= 0, "negative count");
   MRAG_REQUIRE(label >= 0 || label == MRAG_LABEL_DELETED, "label %d invalid", label);
   std::lock_guard<std::mutex> lk(ix->mu);
+  std::unique_lock<std::shared_mutex> wl(ix->rw);
   mrag::DeviceGuard g(ix->device);
   if (n == 0) return MRAG_OK;
   MRAG_REQUIRE(rows != nullptr, "NULL rows");
@@ -2567,9 +2620,17 @@ int mrag_knn_search(mrag_knn_index* ix, const float* queries, int64_t nq, int32_
   MRAG_REQUIRE(label_filter >= MRAG_LABEL_ANY, "label filter %d invalid", label_filter);
   MRAG_REQUIRE(ptr_kind == MRAG_PTR_HOST || ptr_kind == MRAG_PTR_DEVICE, "bad ptr_kind %d", ptr_kind);
   MRAG_REQUIRE(nq < (1 << 24), "too many queries in one call");
-  std::lock_guard<std::mutex> lk(ix->mu);
+  std::shared_lock<std::shared_mutex> rl(ix->rw);
   mrag::DeviceGuard g(ix->device);
   if (nq == 0) return MRAG_OK;
+  SearchCtx* c = nullptr;
+  if (int rc = ctx_get(ix, &c)) return rc;
+  CtxLease lease{ix, c};
+  bool profile;
+  {
+    std::lock_guard<std::mutex> lk(ix->pool_mu);
+    profile = ix->profile;
+  }
   MRAG_REQUIRE(queries && out_scores && out_rows, "NULL query/output pointer");
   hipStream_t s = stream_arg ? (hipStream_t)stream_arg : ix->stream;
   const bool host = ptr_kind == MRAG_PTR_HOST;
@@ -2581,17 +2642,16 @@ int mrag_knn_search(mrag_knn_index* ix, const float* queries, int64_t nq, int32_
   double* os64 = out_scores64;
   int64_t* orr = out_rows;
   if (host) {
-    if (int rc = ensure(ix->out_s, nout * 4)) return rc;
-    if (int rc = ensure(ix->out_r, nout * 8)) return rc;
-    os = (float*)ix->out_s.p;
-    orr = (int64_t*)ix->out_r.p;
+    if (int rc = ensure(c->out_s, nout * 4)) return rc;
+    if (int rc = ensure(c->out_r, nout * 8)) return rc;
+    os = (float*)c->out_s.p;
+    orr = (int64_t*)c->out_r.p;
     if (out_scores64) {
-      if (int rc = ensure(ix->out_s64, nout * 8)) return rc;
-      os64 = (double*)ix->out_s64.p;
+      if (int rc = ensure(c->out_s64, nout * 8)) return rc;
+      os64 = (double*)c->out_s64.p;
     }
   }
-  ix->last_uncertified = 0;
-  ix->last_retries = 0;
+  int64_t uncertified = 0, retries = 0;
 
   auto generic_args = [&]() {
     mrag_knn::GenericSearch ga{};
@@ -2602,9 +2662,9 @@ int mrag_knn_search(mrag_knn_index* ix, const float* queries, int64_t nq, int32_
     ga.n = ix->n;
     ga.D = D;
     ga.DP = DP;
-    ga.q16 = (const _Float16*)ix->q16.p;
-    ga.q32 = (const float*)ix->q32.p;
-    ga.qn = (const double*)ix->qn.p;
+    ga.q16 = (const _Float16*)c->q16.p;
+    ga.q32 = (const float*)c->q32.p;
+    ga.qn = (const double*)c->qn.p;
     ga.nq = (int)nq;
     ga.k = k;
     ga.label_filter = label_filter;
@@ -2623,16 +2683,16 @@ int mrag_knn_search(mrag_knn_index* ix, const float* queries, int64_t nq, int32_
     // K7g (knn_generic.hip): widths and depths the fused scan does not instantiate
     const float* qsrc = queries;
     if (host) {
-      if (int rc = ensure(ix->qin, (size_t)nq * D * 4)) return rc;
-      MRAG_HIP(hipMemcpyAsync(ix->qin.p, queries, (size_t)nq * D * 4, hipMemcpyHostToDevice, s));
-      qsrc = (const float*)ix->qin.p;
+      if (int rc = ensure(c->qin, (size_t)nq * D * 4)) return rc;
+      MRAG_HIP(hipMemcpyAsync(c->qin.p, queries, (size_t)nq * D * 4, hipMemcpyHostToDevice, s));
+      qsrc = (const float*)c->qin.p;
     }
-    if (int rc = ensure(ix->q32, (size_t)nq * DP * 4)) return rc;
-    if (int rc = ensure(ix->qn, (size_t)nq * 8)) return rc;
-    if (int rc = ensure(ix->q16, (size_t)nq * DP * 2)) return rc;
-    if (int rc = launch_prep(qsrc, nq, D, DP, nq, (float*)ix->q32.p, (double*)ix->qn.p, (_Float16*)ix->q16.p, s))
+    if (int rc = ensure(c->q32, (size_t)nq * DP * 4)) return rc;
+    if (int rc = ensure(c->qn, (size_t)nq * 8)) return rc;
+    if (int rc = ensure(c->q16, (size_t)nq * DP * 2)) return rc;
+    if (int rc = launch_prep(qsrc, nq, D, DP, nq, (float*)c->q32.p, (double*)c->qn.p, (_Float16*)c->q16.p, s))
       return rc;
-    if (int rc = mrag_knn::search_generic(generic_args(), ix->gws, s, nullptr)) return rc;
+    if (int rc = mrag_knn::search_generic(generic_args(), c->gws, s, nullptr)) return rc;
   } else {
     // v2 (64 queries/wave, KL = 8) unless k is deep enough to want longer per-lane lists
     // (per-lane lists of 8; for 32 < k <= 64 the union of the S split lists still holds
@@ -2658,46 +2718,46 @@ int mrag_knn_search(mrag_knn_index* ix, const float* queries, int64_t nq, int32_
 
     const float* qsrc = queries;
     if (host) {
-      if (int rc = ensure(ix->qin, (size_t)nq * D * 4)) return rc;
-      MRAG_HIP(hipMemcpyAsync(ix->qin.p, queries, (size_t)nq * D * 4, hipMemcpyHostToDevice, s));
-      qsrc = (const float*)ix->qin.p;
+      if (int rc = ensure(c->qin, (size_t)nq * D * 4)) return rc;
+      MRAG_HIP(hipMemcpyAsync(c->qin.p, queries, (size_t)nq * D * 4, hipMemcpyHostToDevice, s));
+      qsrc = (const float*)c->qin.p;
     }
-    if (int rc = ensure(ix->q32, (size_t)Qp * DP * 4)) return rc;
-    if (int rc = ensure(ix->qn, (size_t)Qp * 8)) return rc;
-    if (int rc = ensure(ix->q16, (size_t)Qp * DP * 2)) return rc;
-    if (int rc = ensure(ix->part_s, (size_t)S * Qp * KL * 4)) return rc;
-    if (int rc = ensure(ix->part_i, (size_t)S * Qp * KL * 4)) return rc;
-    if (int rc = ensure(ix->thresh, (size_t)Qp * 4)) return rc;
-    if (int rc = ensure(ix->fail_list, (size_t)Qp * 4)) return rc;
-    if (int rc = ensure(ix->counters, 16)) return rc;
-    if (int rc = ensure(ix->cand_cnt, (size_t)Qp * 4)) return rc;
-    if (int rc = ensure(ix->theta, (size_t)Qp * 4)) return rc;
+    if (int rc = ensure(c->q32, (size_t)Qp * DP * 4)) return rc;
+    if (int rc = ensure(c->qn, (size_t)Qp * 8)) return rc;
+    if (int rc = ensure(c->q16, (size_t)Qp * DP * 2)) return rc;
+    if (int rc = ensure(c->part_s, (size_t)S * Qp * KL * 4)) return rc;
+    if (int rc = ensure(c->part_i, (size_t)S * Qp * KL * 4)) return rc;
+    if (int rc = ensure(c->thresh, (size_t)Qp * 4)) return rc;
+    if (int rc = ensure(c->fail_list, (size_t)Qp * 4)) return rc;
+    if (int rc = ensure(c->counters, 16)) return rc;
+    if (int rc = ensure(c->cand_cnt, (size_t)Qp * 4)) return rc;
+    if (int rc = ensure(c->theta, (size_t)Qp * 4)) return rc;
     if (use_v3)
-      if (int rc = ensure(ix->part_tau, (size_t)S * Qp * 4)) return rc;
+      if (int rc = ensure(c->part_tau, (size_t)S * Qp * 4)) return rc;
 
-    if (int rc = launch_prep(qsrc, nq, D, DP, Qp, (float*)ix->q32.p, (double*)ix->qn.p, (_Float16*)ix->q16.p, s,
-                             PrepClear{(int32_t*)ix->counters.p, (int32_t*)ix->cand_cnt.p, (uint32_t*)ix->theta.p}))
+    if (int rc = launch_prep(qsrc, nq, D, DP, Qp, (float*)c->q32.p, (double*)c->qn.p, (_Float16*)c->q16.p, s,
+                             PrepClear{(int32_t*)c->counters.p, (int32_t*)c->cand_cnt.p, (uint32_t*)c->theta.p}))
       return rc;
 
     ScanParams sp{};
-    sp.theta = (uint32_t*)ix->theta.p;
+    sp.theta = (uint32_t*)c->theta.p;
 
     sp.x16 = (const _Float16*)ix->x16.p;
     sp.labels = (const int32_t*)ix->labels.p;
-    sp.q16 = (const _Float16*)ix->q16.p;
+    sp.q16 = (const _Float16*)c->q16.p;
     sp.ntiles = ntiles;
     sp.qgroups = qgroups;
     sp.splits = S;
     sp.Qp = (int)Qp;
     sp.label_filter = label_filter;
-    sp.part_s = (float*)ix->part_s.p;
-    sp.part_i = (int32_t*)ix->part_i.p;
-    sp.fail_list = (const int32_t*)ix->fail_list.p;
-    sp.fail_cnt = (const int32_t*)ix->counters.p;
-    sp.thresh = (const float*)ix->thresh.p;
-    sp.cand_cnt = (int32_t*)ix->cand_cnt.p;
+    sp.part_s = (float*)c->part_s.p;
+    sp.part_i = (int32_t*)c->part_i.p;
+    sp.fail_list = (const int32_t*)c->fail_list.p;
+    sp.fail_cnt = (const int32_t*)c->counters.p;
+    sp.thresh = (const float*)c->thresh.p;
+    sp.cand_cnt = (int32_t*)c->cand_cnt.p;
     sp.k = k;
-    sp.part_tau = use_v3 ? (float*)ix->part_tau.p : nullptr;
+    sp.part_tau = use_v3 ? (float*)c->part_tau.p : nullptr;
 
     const bool use_v4 = use_v3 && ix->scan_v4;
     const bool use_v5 = use_v3 && !use_v4 && ix->scan_v5;
@@ -2753,10 +2813,10 @@ int mrag_knn_search(mrag_knn_index* ix, const float* queries, int64_t nq, int32_
                          (int)Qp, k, sp.theta, per);
       MRAG_CHECK_LAUNCH();
     }
-    if (ix->profile) MRAG_HIP(hipEventRecord(ix->ev0, s));
+    if (profile) MRAG_HIP(hipEventRecord(c->ev0, s));
     hipLaunchKernelGGL(scan, sgrid, dim3(use_v4 ? SCAN4_THREADS : use_v2 ? SCAN2_THREADS : SCAN_THREADS), 0, s, sp);
     MRAG_CHECK_LAUNCH();
-    if (ix->profile) MRAG_HIP(hipEventRecord(ix->ev1, s));
+    if (profile) MRAG_HIP(hipEventRecord(c->ev1, s));
     sp.ntiles = ntiles;  // 64-row tiles for the collect pass
 
     MergeParams mp{};
@@ -2770,8 +2830,8 @@ int mrag_knn_search(mrag_knn_index* ix, const float* queries, int64_t nq, int32_
     mp.M = M;
     mp.R = R;
     mp.Mp = Mp;
-    mp.q32 = (const float*)ix->q32.p;
-    mp.qn = (const double*)ix->qn.p;
+    mp.q32 = (const float*)c->q32.p;
+    mp.qn = (const double*)c->qn.p;
     mp.x32 = (const float*)ix->x32.p;
     mp.xn = (const double*)ix->xn.p;
     mp.D = D;
@@ -2780,10 +2840,10 @@ int mrag_knn_search(mrag_knn_index* ix, const float* queries, int64_t nq, int32_
     mp.out_s64 = os64;
     mp.out_r = orr;
     mp.row_offset = row_offset;
-    mp.thresh = (float*)ix->thresh.p;
-    mp.fail_list = (int32_t*)ix->fail_list.p;
-    mp.fail_cnt = (int32_t*)ix->counters.p;
-    mp.theta = (const uint32_t*)ix->theta.p;
+    mp.thresh = (float*)c->thresh.p;
+    mp.fail_list = (int32_t*)c->fail_list.p;
+    mp.fail_cnt = (int32_t*)c->counters.p;
+    mp.theta = (const uint32_t*)c->theta.p;
     mp.part_tau = sp.part_tau;
     // K8 key selection: the best M + 1 keys (the M candidates and the first one left out) by
     // the register top-64P fold when they fit, else the full bitonic sort (env MRAG_K8_SORT=1
@@ -2805,9 +2865,9 @@ int mrag_knn_search(mrag_knn_index* ix, const float* queries, int64_t nq, int32_
       // ccap near-duplicates within eps of its k-th score) sends the batch to K7g below,
       // whose per-query storage is sized from a histogram — nothing grows across searches
       const int ccap = (int)std::max<int64_t>(256, std::min<int64_t>(4096, ((int64_t)64 << 20) / Qp));
-      if (int rc = ensure(ix->cand, (size_t)Qp * ccap * 4)) return rc;
-      if (int rc = ensure(ix->scratch, (size_t)Qp * ccap * 8)) return rc;
-      sp.cand = (int32_t*)ix->cand.p;
+      if (int rc = ensure(c->cand, (size_t)Qp * ccap * 4)) return rc;
+      if (int rc = ensure(c->scratch, (size_t)Qp * ccap * 8)) return rc;
+      sp.cand = (int32_t*)c->cand.p;
       sp.ccap = ccap;
       hipLaunchKernelGGL(collect, sgrid, dim3(SCAN_THREADS), 0, s, sp);
       MRAG_CHECK_LAUNCH();
@@ -2817,7 +2877,7 @@ int mrag_knn_search(mrag_knn_index* ix, const float* queries, int64_t nq, int32_
       fp.cand_cnt = sp.cand_cnt;
       fp.cand = sp.cand;
       fp.ccap = ccap;
-      fp.scratch = (double*)ix->scratch.p;
+      fp.scratch = (double*)c->scratch.p;
       fp.q32 = mp.q32;
       fp.qn = mp.qn;
       fp.x32 = mp.x32;
@@ -2829,21 +2889,22 @@ int mrag_knn_search(mrag_knn_index* ix, const float* queries, int64_t nq, int32_
       fp.out_s64 = os64;
       fp.out_r = orr;
       fp.row_offset = row_offset;
-      fp.overflow = (int32_t*)ix->counters.p + 1;
+      fp.overflow = (int32_t*)c->counters.p + 1;
       hipLaunchKernelGGL(knn_final_kernel, dim3((unsigned)nq), dim3(MERGE_THREADS), (size_t)DP * 4, s, fp);
       MRAG_CHECK_LAUNCH();
-      MRAG_HIP(hipMemcpyAsync(ix->host_counters, ix->counters.p, 8, hipMemcpyDeviceToHost, s));
-      if (int rc = wait_stream(ix, s)) return rc;
-      ix->last_uncertified = ix->host_counters[0];
-      if (ix->profile) {
+      MRAG_HIP(hipMemcpyAsync(c->host_counters, c->counters.p, 8, hipMemcpyDeviceToHost, s));
+      if (int rc = wait_stream(c, s)) return rc;
+      uncertified = c->host_counters[0];
+      if (profile) {
         float ms = 0.f;
-        MRAG_HIP(hipEventElapsedTime(&ms, ix->ev0, ix->ev1));
+        MRAG_HIP(hipEventElapsedTime(&ms, c->ev0, c->ev1));
+        std::lock_guard<std::mutex> lk(ix->pool_mu);
         ix->scan_ms += ms;
         ix->scan_launches++;
       }
-      if (ix->host_counters[1] != 0) {
-        ix->last_retries = 1;
-        if (int rc = mrag_knn::search_generic(generic_args(), ix->gws, s, nullptr)) return rc;
+      if (c->host_counters[1] != 0) {
+        retries = 1;
+        if (int rc = mrag_knn::search_generic(generic_args(), c->gws, s, nullptr)) return rc;
       }
     }
   }
@@ -2853,7 +2914,11 @@ int mrag_knn_search(mrag_knn_index* ix, const float* queries, int64_t nq, int32_
     MRAG_HIP(hipMemcpyAsync(out_rows, orr, nout * 8, hipMemcpyDeviceToHost, s));
     if (out_scores64) MRAG_HIP(hipMemcpyAsync(out_scores64, os64, nout * 8, hipMemcpyDeviceToHost, s));
   }
-  return wait_stream(ix, s);
+  if (int rc = wait_stream(c, s)) return rc;
+  std::lock_guard<std::mutex> lk(ix->pool_mu);
+  ix->last_uncertified = uncertified;
+  ix->last_retries = retries;
+  return MRAG_OK;
 }
 
 int mrag_topk_merge(const double* scores64, const int64_t* rows, int32_t nlists, int64_t nq, int32_t k,

@@ -310,3 +310,51 @@ def test_k11_matches_restatement(cuda):
         np.testing.assert_array_equal(gr.cpu().numpy(), er)
         np.testing.assert_array_equal(g64.cpu().numpy(), e64)
         np.testing.assert_array_equal(gs.cpu().numpy(), es)
+
+
+def test_concurrent_searches_own_streams(cuda):
+    """Several host threads searching ONE index at once, each on its own stream (the library
+    gives every search its own workspace; bench.py keeps two in flight): every result equals
+    the serial search bit for bit and the oracle; clustered data sends some queries through
+    the collect pass while other searches run; an add between rounds is seen by the next one."""
+    import threading
+
+    import torch
+
+    from app.vector_store import FlatIndex
+
+    x = clustered_corpus(30000, 256, 21, n_clusters=40)
+    ix = FlatIndex(256)
+    ix.add(x)
+    qs = [unit_rows(300, 256, 100 + i) for i in range(4)] + [x[:200] + np.float32(1e-3)]
+    serial = [ix.search(torch.from_numpy(q).to(cuda), 10) for q in qs]
+    serial = [(s.cpu().numpy(), r.cpu().numpy()) for s, r in serial]
+    for i, q in enumerate(qs):
+        os_, or_ = flat_cosine_topk(x, np.zeros(len(x)), q, 10)
+        _check(serial[i][0], serial[i][1], os_, or_)
+    for rnd in range(3):
+        out = [None] * len(qs)
+        errs = []
+
+        def work(i):
+            try:
+                st = torch.cuda.Stream(device=cuda)
+                with torch.cuda.stream(st):
+                    s, r = ix.search(torch.from_numpy(qs[i]).to(cuda), 10)
+                    out[i] = (s.cpu().numpy(), r.cpu().numpy())
+            except Exception as e:  # surfaced below
+                errs.append(e)
+
+        th = [threading.Thread(target=work, args=(i,)) for i in range(len(qs))]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(timeout=120)
+        assert not errs, errs
+        for i in range(len(qs)):
+            np.testing.assert_array_equal(out[i][1], serial[i][1])
+            np.testing.assert_array_equal(out[i][0], serial[i][0])
+    extra = unit_rows(10, 256, 99)
+    ix.add(extra)
+    s, r = ix.search(torch.from_numpy(extra).to(cuda), 1)
+    assert (r.cpu().numpy()[:, 0] == np.arange(30000, 30010)).all()
