@@ -69,7 +69,8 @@ struct mrag_encoder {
   std::vector<std::string> expected;
   // workspace
   Buf X, H16, QKV, ATT, F16, PATCH, IMG, IDS, MASK, TYPES, ROWS, POOL16, OUT;
-  int64_t ws_tokens = 0;
+  Buf XG, AG, HG, FG;  // the pooled rows of a CLIP tower's last layer (clip_layer_pooled)
+  int64_t ws_tokens = 0, ws_batch = 0;
   // Device-pointer calls return without a host sync (stream-ordered, like any kernel launch):
   // `done` marks the end of the last call's work on `last_stream`; a call on another stream
   // first waits for it (the workspace is shared), and a workspace reallocation first
@@ -222,10 +223,18 @@ int layer_index(const std::string& name, const std::string& marker) {
 
 int ensure_workspace(mrag_encoder* e, int B, int T) {
   const int64_t tokens = (int64_t)B * T;
-  if (tokens <= e->ws_tokens) return MRAG_OK;
+  if (tokens <= e->ws_tokens && B <= e->ws_batch) return MRAG_OK;
   if (e->last_stream) MRAG_HIP(hipEventSynchronize(e->done));  // in-flight work still reads the old buffers
   const auto& c = e->cfg;
   const int64_t D = c.hidden, I = c.intermediate;
+  if (B > e->ws_batch) {  // pooled rows of the last CLIP layer (clip_layer_pooled)
+    if (int rc = buf_ensure(e->XG, (size_t)B * D * 4)) return rc;
+    if (int rc = buf_ensure(e->AG, (size_t)B * D * 2)) return rc;
+    if (int rc = buf_ensure(e->HG, (size_t)B * D * 2)) return rc;
+    if (int rc = buf_ensure(e->FG, (size_t)B * I * 2)) return rc;
+    e->ws_batch = B;
+  }
+  if (tokens <= e->ws_tokens) return MRAG_OK;
   if (int rc = buf_ensure(e->X, tokens * D * 4)) return rc;
   if (int rc = buf_ensure(e->H16, tokens * D * 2)) return rc;
   if (int rc = buf_ensure(e->QKV, tokens * 3 * D * 2)) return rc;
@@ -300,6 +309,50 @@ int clip_layer(mrag_encoder* e, const Layer& L, int B, int T, const int32_t* mas
   const int act = c.act == 0 ? EPI_F16_QUICK_GELU : EPI_F16_GELU_ERF;
   if (int rc = gemm(H, L.w1.p, L.b1.p, e->F16.p, M, I, D, I, act, s)) return rc;
   return gemm(e->F16.p, L.w2.p, L.b2.p, X, M, D, I, D, EPI_F32_RESIDUAL, s);
+}
+
+// The LAST pre-LN layer of a tower that pools one row per sequence (CLIP: the class token of
+// an image, the EOS token of a text): every row's LN1 / q|k|v / attention as in clip_layer (the
+// pooled row attends to all of them), then out-proj, LN2 and the MLP only on the B pooled rows
+// `rows`, gathered into XG (f32 residual) / AG (attention output). A GEMM row, a LayerNorm row
+// and the residual add depend only on that row (every GEMM kernel accumulates in one order
+// whatever M selects it), so the pooled rows are bit-identical to the full layer's (env
+// MRAG_ENC_FULL_LAST=1 runs the full layer: A/B check in scripts/enc_dump.py). ViT-B/32 at
+// B = 256: the layer's out-proj / fc1 / fc2 run on 256 rows instead of 12,800.
+int clip_layer_pooled(mrag_encoder* e, const Layer& L, int B, int T, const int32_t* mask, int causal, const int* rows,
+                      hipStream_t s) {
+  const auto& c = e->cfg;
+  const int D = c.hidden, I = c.intermediate, M = B * T;
+  float* X = (float*)e->X.p;
+  _Float16* H = (_Float16*)e->H16.p;
+  if (int rc = layernorm(X, nullptr, nullptr, H, L.ln1g, L.ln1b, M, D, c.ln_eps, s)) return rc;
+  if (int rc = gemm(H, L.wqkv.p, L.bqkv.p, e->QKV.p, M, 3 * D, D, 3 * D, EPI_F16, s)) return rc;
+  AttentionArgs a{};
+  a.qkv = (const _Float16*)e->QKV.p;
+  a.out = (_Float16*)e->ATT.p;
+  a.mask = mask;
+  a.B = B;
+  a.L = T;
+  a.H = c.heads;
+  a.causal = causal;
+  a.scale = 1.0f / sqrtf((float)(D / c.heads));
+  if (int rc = launch_attention(a, D / c.heads, s)) return rc;
+  if (int rc = launch_gather_rows(X, e->XG.p, rows, B, D * 4, s)) return rc;
+  if (int rc = launch_gather_rows(e->ATT.p, e->AG.p, rows, B, D * 2, s)) return rc;
+  float* XG = (float*)e->XG.p;
+  if (int rc = gemm(e->AG.p, L.wo.p, L.bo.p, XG, B, D, D, D, EPI_F32_RESIDUAL, s)) return rc;
+  if (int rc = layernorm(XG, nullptr, nullptr, (_Float16*)e->HG.p, L.ln2g, L.ln2b, B, D, c.ln_eps, s)) return rc;
+  const int act = c.act == 0 ? EPI_F16_QUICK_GELU : EPI_F16_GELU_ERF;
+  if (int rc = gemm(e->HG.p, L.w1.p, L.b1.p, e->FG.p, B, I, D, I, act, s)) return rc;
+  return gemm(e->FG.p, L.w2.p, L.b2.p, XG, B, D, I, D, EPI_F32_RESIDUAL, s);
+}
+
+bool full_last_layer() {
+  static const bool v = [] {
+    const char* e = getenv("MRAG_ENC_FULL_LAST");
+    return e && atoi(e) == 1;
+  }();
+  return v;
 }
 
 // Post-LN transformer layer (BERT): X = LN(X + attn(X)); X = LN(X + ffn(X)).
@@ -391,7 +444,7 @@ int mrag_encoder_destroy(mrag_encoder* e) {
     for (Buf* b : {&e->patch_w, &e->cls, &e->pos, &e->pre_g, &e->pre_b, &e->post_g, &e->post_b, &e->proj_w, &e->tok,
                    &e->type0, &e->emb_g, &e->emb_b, &e->X, &e->H16, &e->QKV, &e->ATT, &e->F16, &e->PATCH, &e->IMG,
                    &e->IDS, &e->MASK, &e->ROWS, &e->POOL16, &e->OUT, &e->pool_w, &e->pool_b, &e->cls_w, &e->cls_b,
-                   &e->POOL32, &e->TYPES})
+                   &e->POOL32, &e->TYPES, &e->XG, &e->AG, &e->HG, &e->FG})
       buf_free(*b);
     (void)hipStreamDestroy(e->stream);
   }
@@ -541,11 +594,17 @@ int mrag_encoder_embed_images(mrag_encoder* e, const uint8_t* images, int32_t ba
   if (int rc = launch_vit_embed_ln((const float*)e->PATCH.p, (const float*)e->cls.p, (const float*)e->pos.p,
                                    (const float*)e->pre_g.p, (const float*)e->pre_b.p, X, B, T, D, c.ln_eps, s))
     return rc;
-  for (int i = 0; i < c.layers; ++i)
-    if (int rc = clip_layer(e, e->layers[i], B, T, nullptr, 0, s)) return rc;
   if (int rc = launch_cls_rows(B, T, (int*)e->ROWS.p, s)) return rc;
-  if (int rc = layernorm(X, (const int*)e->ROWS.p, nullptr, (_Float16*)e->POOL16.p, e->post_g, e->post_b, B, D,
-                         c.ln_eps, s))
+  const bool prune = !full_last_layer() && c.layers > 0;
+  for (int i = 0; i < c.layers; ++i) {
+    if (prune && i == c.layers - 1) {
+      if (int rc = clip_layer_pooled(e, e->layers[i], B, T, nullptr, 0, (const int*)e->ROWS.p, s)) return rc;
+    } else if (int rc = clip_layer(e, e->layers[i], B, T, nullptr, 0, s)) {
+      return rc;
+    }
+  }
+  if (int rc = layernorm(prune ? (const float*)e->XG.p : X, prune ? nullptr : (const int*)e->ROWS.p, nullptr,
+                         (_Float16*)e->POOL16.p, e->post_g, e->post_b, B, D, c.ln_eps, s))
     return rc;
   float* dst = out;
   if (ptr_kind == MRAG_PTR_HOST) {
@@ -602,11 +661,17 @@ int mrag_encoder_embed_tokens(mrag_encoder* e, const int32_t* ids, const int32_t
     if (int rc = launch_token_embed(dids, (const float*)e->tok.p, (const float*)e->pos.p, nullptr, nullptr, X, B, T, D,
                                     c.vocab, s))
       return rc;
-    for (int i = 0; i < c.layers; ++i)
-      if (int rc = clip_layer(e, e->layers[i], B, T, dmask, 1, s)) return rc;
     if (int rc = launch_eos_rows(dids, B, T, c.eos_token_id, (int*)e->ROWS.p, s)) return rc;
-    if (int rc = layernorm(X, (const int*)e->ROWS.p, nullptr, (_Float16*)e->POOL16.p, e->post_g, e->post_b, B, D,
-                           c.ln_eps, s))
+    const bool prune = !full_last_layer() && c.layers > 0;
+    for (int i = 0; i < c.layers; ++i) {
+      if (prune && i == c.layers - 1) {
+        if (int rc = clip_layer_pooled(e, e->layers[i], B, T, dmask, 1, (const int*)e->ROWS.p, s)) return rc;
+      } else if (int rc = clip_layer(e, e->layers[i], B, T, dmask, 1, s)) {
+        return rc;
+      }
+    }
+    if (int rc = layernorm(prune ? (const float*)e->XG.p : X, prune ? nullptr : (const int*)e->ROWS.p, nullptr,
+                           (_Float16*)e->POOL16.p, e->post_g, e->post_b, B, D, c.ln_eps, s))
       return rc;
     if (int rc = gemm(e->POOL16.p, e->proj_w.p, nullptr, dst, B, c.proj_dim, D, c.proj_dim, EPI_F32, s)) return rc;
   } else {

@@ -58,6 +58,7 @@ int launch_cls_head(const float* pooled, const float* Wc, const float* bc, float
                     hipStream_t s);
 int launch_eos_rows(const int32_t* ids, int B, int T, int eos_id, int* rows, hipStream_t s);
 int launch_cls_rows(int B, int T, int* rows, hipStream_t s);
+int launch_gather_rows(const void* src, void* dst, const int* rows, int B, int row_bytes, hipStream_t s);
 int launch_mean_pool(const float* X, const int32_t* mask, float* out, int B, int T, int D, hipStream_t s);
 
 }  // namespace mrag_enc

@@ -2115,6 +2115,27 @@ int launch_eos_rows(const int32_t* ids, int B, int T, int eos_id, int* rows, hip
   return MRAG_OK;
 }
 
+// dst[b] = src[rows[b]] for row_bytes-byte rows (row_bytes % 16 == 0): the pooled rows of a
+// CLIP tower's last layer (cls / eos) gathered into a compact batch
+__global__ __launch_bounds__(256) void gather_rows_kernel(const char* __restrict__ src, char* __restrict__ dst,
+                                                           const int* __restrict__ rows, int B, int row_bytes) {
+  const int chunks = row_bytes >> 4;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (int64_t)B * chunks) return;
+  const int b = (int)(i / chunks), c = (int)(i - (int64_t)b * chunks);
+  ((f32x4*)(dst + (size_t)b * row_bytes))[c] = ((const f32x4*)(src + (size_t)rows[b] * row_bytes))[c];
+}
+
+int launch_gather_rows(const void* src, void* dst, const int* rows, int B, int row_bytes, hipStream_t s) {
+  if (B <= 0) return MRAG_OK;
+  MRAG_REQUIRE(row_bytes % 16 == 0, "gather_rows: row bytes %d not a multiple of 16", row_bytes);
+  const int64_t n = (int64_t)B * (row_bytes / 16);
+  hipLaunchKernelGGL(gather_rows_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, (const char*)src,
+                     (char*)dst, rows, B, row_bytes);
+  MRAG_CHECK_LAUNCH();
+  return MRAG_OK;
+}
+
 int launch_cls_rows(int B, int T, int* rows, hipStream_t s) {
   if (B == 0) return MRAG_OK;
   hipLaunchKernelGGL(cls_rows_kernel, dim3((unsigned)((B + 63) / 64)), dim3(64), 0, s, B, T, rows);
