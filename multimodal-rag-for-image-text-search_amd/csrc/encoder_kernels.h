@@ -23,6 +23,7 @@ struct GemmArgs {
   // partial-accumulator slots, and one arrival counter per output tile (zero between launches)
   float* sk_part;
   int* sk_cnt;
+  int k3_remap;  // K3: XCD-contiguous tile order (set by the launcher)
 };
 
 struct LayerNormArgs {

@@ -151,8 +151,12 @@ __global__ __launch_bounds__(GTHREADS) void gemm_nt_kernel(GemmArgs g) {
   const uint32_t lds_base = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)((AS3 char*)smem));
 
   const int tiles_n = g.N / GN;
-  // consecutive blocks walk N for a fixed M panel (the A panel stays L2-resident)
-  const int tm = blockIdx.x / tiles_n, tn = blockIdx.x - (blockIdx.x / tiles_n) * tiles_n;
+  // consecutive tile ids walk N for a fixed M panel; blocks b, b + 8, ... (one XCD under the
+  // round-robin dispatch) take consecutive tile ids (xcd_remap), so the tiles_n tiles of an A
+  // panel are fetched into ONE XCD's L2 instead of being dealt over tiles_n XCDs (speed only;
+  // env MRAG_K3_REMAP=0 keeps the plain order for A/B timing)
+  const int T = g.k3_remap ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+  const int tm = T / tiles_n, tn = T - (T / tiles_n) * tiles_n;
   const int m0 = tm * GM, n0 = tn * GN;
   const int ksteps = g.K / GK;
 
@@ -1932,12 +1936,18 @@ int launch_gemm(const GemmArgs& g, int epi, hipStream_t s) {
     if (cfg == 1) return launch_gemm_8p_cfg<1>(g, epi, s);
   }
   const dim3 grid((unsigned)(((g.M + GM - 1) / GM) * (g.N / GN)));
+  static const int k3_remap = [] {
+    const char* e = getenv("MRAG_K3_REMAP");
+    return e ? atoi(e) : 1;
+  }();
+  GemmArgs g3 = g;
+  g3.k3_remap = k3_remap;
   switch (epi) {
-    case EPI_F16: hipLaunchKernelGGL(gemm_nt_kernel<EPI_F16>, grid, dim3(GTHREADS), 0, s, g); break;
-    case EPI_F16_QUICK_GELU: hipLaunchKernelGGL(gemm_nt_kernel<EPI_F16_QUICK_GELU>, grid, dim3(GTHREADS), 0, s, g); break;
-    case EPI_F16_GELU_ERF: hipLaunchKernelGGL(gemm_nt_kernel<EPI_F16_GELU_ERF>, grid, dim3(GTHREADS), 0, s, g); break;
-    case EPI_F32_RESIDUAL: hipLaunchKernelGGL(gemm_nt_kernel<EPI_F32_RESIDUAL>, grid, dim3(GTHREADS), 0, s, g); break;
-    case EPI_F32: hipLaunchKernelGGL(gemm_nt_kernel<EPI_F32>, grid, dim3(GTHREADS), 0, s, g); break;
+    case EPI_F16: hipLaunchKernelGGL(gemm_nt_kernel<EPI_F16>, grid, dim3(GTHREADS), 0, s, g3); break;
+    case EPI_F16_QUICK_GELU: hipLaunchKernelGGL(gemm_nt_kernel<EPI_F16_QUICK_GELU>, grid, dim3(GTHREADS), 0, s, g3); break;
+    case EPI_F16_GELU_ERF: hipLaunchKernelGGL(gemm_nt_kernel<EPI_F16_GELU_ERF>, grid, dim3(GTHREADS), 0, s, g3); break;
+    case EPI_F32_RESIDUAL: hipLaunchKernelGGL(gemm_nt_kernel<EPI_F32_RESIDUAL>, grid, dim3(GTHREADS), 0, s, g3); break;
+    case EPI_F32: hipLaunchKernelGGL(gemm_nt_kernel<EPI_F32>, grid, dim3(GTHREADS), 0, s, g3); break;
     default: return mrag::fail(MRAG_ERR_ARG, "gemm: bad epilogue %d", epi);
   }
   MRAG_CHECK_LAUNCH();
