@@ -1747,7 +1747,11 @@ bool k3_beats_k3d(const GemmArgs& g) {
   const long cus = std::max(8, num_cus() / 8 * 8);
   const long t256 = (long)((g.M + 255) / 256) * (g.N / 256), t128 = (long)((g.M + 127) / 128) * (g.N / 128);
   const long r_d = (t256 + cus - 1) / cus, r_3 = (t128 + 2 * cus - 1) / (2 * cus);
-  return 2 * r_3 < 3 * r_d;  // K3 time ~ (2/3) r_3 < r_d; ties stay on K3d
+  static const bool tie_k3 = [] {  // env MRAG_GEMM_TIE_K3=1: ties go to K3 (A/B timing)
+    const char* e = getenv("MRAG_GEMM_TIE_K3");
+    return e && atoi(e) == 1;
+  }();
+  return tie_k3 ? 2 * r_3 <= 3 * r_d : 2 * r_3 < 3 * r_d;  // K3 time ~ (2/3) r_3 < r_d; ties stay on K3d
 }
 
 // K3d stream-K (SK) policy: env MRAG_G8_SK = 0 (default) off, 1 where the estimate says it
