@@ -1668,11 +1668,26 @@ __global__ __launch_bounds__(64) void theta_init_kernel(const float* __restrict_
   constexpr int PER_LANE = 16;  // nvals = per * splits <= 4 * 256
   const int q = blockIdx.x, lane = threadIdx.x;
   float v[PER_LANE];
+  // lane l takes splits l, l + 64, ... whole (one 16-byte load for per = 4, 8 bytes for per = 2):
+  // the (split, query) groups are Qp * per floats apart, so per-value loads touched a line each;
+  // the k-th largest does not depend on which lane holds a value
+  const int splits = nvals / per;
 #pragma unroll
-  for (int t = 0; t < PER_LANE; ++t) {
-    const int i = lane + 64 * t;
-    // value i = (split i / per, part i % per); per = 2 (v2 / v4 / v5 pre-pass) or 4 (v3)
-    v[t] = i < nvals ? smax[((size_t)(i / per) * Qp + q) * per + (i % per)] : -INFINITY;
+  for (int t = 0; t < 4; ++t) {
+    const int sp = lane + 64 * t;
+    const float* src = smax + ((size_t)sp * Qp + q) * per;
+    if (per == 4) {
+      const f32x4 x = sp < splits ? *(const f32x4*)src : f32x4{-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[4 * t + u] = x[u];
+    } else {
+      typedef float f32x2 __attribute__((ext_vector_type(2)));
+      const f32x2 x = sp < splits ? *(const f32x2*)src : f32x2{-INFINITY, -INFINITY};
+      v[4 * t] = x[0];
+      v[4 * t + 1] = x[1];
+      v[4 * t + 2] = -INFINITY;
+      v[4 * t + 3] = -INFINITY;
+    }
   }
   float kth = -INFINITY;
   for (int r = 0; r < k; ++r) {
