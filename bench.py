@@ -197,7 +197,10 @@ def clip_leg(steps: int, warmup: int):
         from app.encoders import bench_clip_images
     except Exception:
         return None
-    return bench_clip_images(steps=steps, warmup=warmup)
+    out = bench_clip_images(steps=steps, warmup=warmup)  # three batches in flight
+    one = bench_clip_images(steps=steps, warmup=warmup, inflight=1)
+    out["one_batch_in_flight"] = {"images_per_s": one["value"], "ms_per_batch": one["ms_per_batch"]}
+    return out
 
 
 FUSION_ROWS_PER_GPU = 1 << 19  # config 5: 4M text + 4M image rows over 8 GPUs
@@ -314,9 +317,6 @@ def fusion_leg(world: int, rank: int, local: int, steps: int, warmup: int):
     ids_m, mask, ids_c = _fusion_queries(dev, NQ)
     per = (NQ + world - 1) // world
     lo, hi = rank * per, min(NQ, (rank + 1) * per)
-    minilm = GpuEncoder(MINILM_L6, device=local)
-    clipt = GpuEncoder(CLIP_TEXT_B32, device=local)
-
     def gather(v):
         if world == 1:
             return v
@@ -326,60 +326,95 @@ def fusion_leg(world: int, rank: int, local: int, steps: int, warmup: int):
         dist.all_gather_into_tensor(out, buf)
         return out[:NQ]
 
-    # the leg runs on its own stream: device-pointer encoder calls are then stream-ordered
-    # (no host sync per call; on the default stream the library synchronises every call). The
-    # text branch (MiniLM -> text search) and the image branch (CLIP text -> image search) are
-    # independent until the fusion; on one GPU the image branch runs in a second host thread
-    # on a second stream (a search returns to the host once its certificate is read, which
-    # would otherwise serialise the branches), so each branch's kernels that leave CUs idle
-    # (attention, LayerNorm, K8, partial GEMM rounds) overlap with the other's. At N > 1 the
-    # branches stay in one thread: their collectives share one communicator and must be issued
-    # in the same order on every rank. MRAG_FUSION_STREAMS=1 serialises them (A/B timing).
-    leg_stream = torch.cuda.Stream(device=dev)
+    # The leg runs on its own streams: device-pointer encoder calls are then stream-ordered (no
+    # host sync per call; on the default stream the library synchronises every call). The text
+    # branch (MiniLM -> text search) and the image branch (CLIP text -> image search) are
+    # independent until the fusion; on one GPU the image branch runs in a second host thread on
+    # a second stream (a search returns to the host once its certificate is read, which would
+    # otherwise serialise the branches), and `slots` steps are in flight at once, each slot with
+    # its own encoder handles (workspaces) and streams (the indexes give every search its own
+    # workspace), so kernels that leave CUs idle (attention, LayerNorm, K8, partial GEMM rounds)
+    # overlap with other branches' and steps' work, as a serving process with concurrent query
+    # batches runs them. At N > 1 everything stays in one thread: the collectives share one
+    # communicator and must be issued in the same order on every rank. MRAG_FUSION_STREAMS=1
+    # serialises the branches, MRAG_FUSION_INFLIGHT sets the steps in flight (A/B timing).
     two = world == 1 and os.environ.get("MRAG_FUSION_STREAMS", "2") != "1"
-    img_stream = torch.cuda.Stream(device=dev) if two else leg_stream
-    pool = None
-    if two:
-        from concurrent.futures import ThreadPoolExecutor
+    slots = max(1, int(os.environ.get("MRAG_FUSION_INFLIGHT", "2"))) if two else 1
+    from concurrent.futures import ThreadPoolExecutor
 
-        pool = ThreadPoolExecutor(max_workers=1)
+    class Slot:
+        def __init__(self):
+            self.minilm = GpuEncoder(MINILM_L6, device=local)
+            self.clipt = GpuEncoder(CLIP_TEXT_B32, device=local)
+            self.leg = torch.cuda.Stream(device=dev)
+            self.img = torch.cuda.Stream(device=dev) if two else self.leg
+            self.pool = ThreadPoolExecutor(max_workers=1) if two else None
 
-    def image_branch():
-        with torch.cuda.stream(img_stream):
-            iv = gather(clipt.embed_tokens(ids_c[lo:hi]))
-            return img_sh.search(iv, ki)
+        def image_branch(self):
+            with torch.cuda.stream(self.img):
+                iv = gather(self.clipt.embed_tokens(ids_c[lo:hi]))
+                return img_sh.search(iv, ki)
 
-    def step():
-        if pool is not None:
-            img_stream.wait_stream(leg_stream)  # the previous step's fusion read its outputs
-            fut = pool.submit(image_branch)
-        else:
-            si, ri = image_branch()
-        tv = gather(minilm.embed_tokens(ids_m[lo:hi], mask[lo:hi]))
-        st, rt = text_sh.search(tv, kt)
-        if pool is not None:
-            si, ri = fut.result()
-            leg_stream.wait_stream(img_stream)
-        if rank == 0:
-            pick, _ = fuse_scores_gpu(st, si, final_n)
-            return pick.cpu()
-        return None
+        def step(self):
+            with torch.cuda.stream(self.leg):
+                if self.pool is not None:
+                    self.img.wait_stream(self.leg)  # the previous step's fusion read its outputs
+                    fut = self.pool.submit(self.image_branch)
+                else:
+                    si, ri = self.image_branch()
+                tv = gather(self.minilm.embed_tokens(ids_m[lo:hi], mask[lo:hi]))
+                st, rt = text_sh.search(tv, kt)
+                if self.pool is not None:
+                    si, ri = fut.result()
+                    self.leg.wait_stream(self.img)
+                if rank == 0:
+                    pick, _ = fuse_scores_gpu(st, si, final_n)
+                    return pick.cpu()
+                return None
+
+    slot_list = [Slot() for _ in range(slots)]
+    runner = ThreadPoolExecutor(max_workers=slots) if slots > 1 else None
+    last = [None]
+
+    def run(nsteps):
+        if runner is None:
+            for _ in range(nsteps):
+                last[0] = slot_list[0].step()
+            return
+
+        def share(j):
+            out = None
+            for _ in range(nsteps // slots + (1 if j < nsteps % slots else 0)):
+                out = slot_list[j].step()
+            return out
+
+        outs = list(runner.map(share, range(slots)))
+        last[0] = next((o for o in outs if o is not None), last[0])
 
     torch.cuda.synchronize()
-    with torch.cuda.stream(leg_stream):
-        for _ in range(warmup):
-            step()
-        torch.cuda.synchronize()
-        _barrier(world)
+    run(max(warmup, slots))
+    torch.cuda.synchronize()
+    _barrier(world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    run(steps)
+    torch.cuda.synchronize()
+    _barrier(world)
+    dt = _max_over_ranks(time.perf_counter() - t0, world)
+    pick = last[0]
+    one_dt = None
+    if runner is not None:  # the one-step-at-a-time rate (branches still on two streams)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(steps):
-            pick = step()
+            slot_list[0].step()
         torch.cuda.synchronize()
-        _barrier(world)
-        dt = _max_over_ranks(time.perf_counter() - t0, world)
-    if pool is not None:
-        pool.shutdown()
+        one_dt = time.perf_counter() - t0
+    for sl in slot_list:
+        if sl.pool is not None:
+            sl.pool.shutdown()
+    if runner is not None:
+        runner.shutdown()
     if rank != 0:
         return None
     fl = fusion_flops_per_query(world)
@@ -395,6 +430,9 @@ def fusion_leg(world: int, rank: int, local: int, steps: int, warmup: int):
                     f"{FUSION_ROWS_PER_GPU} x 512 image rows per GPU ({world * FUSION_ROWS_PER_GPU} + "
                     f"{world * FUSION_ROWS_PER_GPU} total), synthetic weights, rerank off",
         "top_k": {"text": kt, "image": ki, "final_n": final_n},
+        "steps_in_flight": slots,
+        "one_step_in_flight": None if one_dt is None else {"queries_per_s": round(NQ * steps / one_dt, 1),
+                                                          "ms_per_step": round(one_dt / steps * 1e3, 3)},
         "fused_hits_last_step": int((pick >= 0).sum()),
         "roofline": {"bound": "mfma", "scope": "whole step (towers + both scans; fusion and copies add no FLOP)",
                      "achieved": round(achieved, 2), "peak": MFMA_FP16_PEAK_TFLOPS, "unit": "TFLOP/s",
