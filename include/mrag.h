@@ -97,7 +97,11 @@ int mrag_knn_size(const mrag_knn_index* index, int64_t* n);
  * [nq, k]; row ids are offset by `row_offset` (a shard's first global row).
  * Slots past the number of matching rows get score -inf and row -1.
  * out_scores64 (optional, may be NULL) receives the f64 scores used for the
- * ordering — the sharded merge needs them. All data pointers share ptr_kind. */
+ * ordering — the sharded merge needs them. All data pointers share ptr_kind.
+ * Returns once the search's device work is done (it reads back its certificate).
+ * Thread-safe: several host threads may search one index at once, each on its
+ * own stream (every call takes its own search workspace from the index's pool;
+ * add / set_labels wait for searches in flight and exclude new ones). */
 int mrag_knn_search(mrag_knn_index* index, const float* queries, int64_t nq, int32_t k,
                     int32_t label_filter, int64_t row_offset, float* out_scores,
                     double* out_scores64, int64_t* out_rows, int32_t ptr_kind, void* stream);
