@@ -601,7 +601,7 @@ def main():
             },
         }
         if not args.no_clip:
-            clip = clip_leg(steps=max(5, args.steps // 2), warmup=2)  # single-GPU leg, rank 0
+            clip = clip_leg(steps=max(30, args.steps), warmup=3)  # single-GPU leg, rank 0; 30+ batches: three in flight reach steady state
             if clip is not None:
                 if not args.no_cpu_baseline:
                     clip["cpu_baseline"] = clip_cpu_baseline()
