@@ -555,7 +555,7 @@ def main():
         del sharded
         index.close()
         torch.cuda.empty_cache()
-        fusion = fusion_leg(world, rank, local, steps=max(5, args.steps // 2), warmup=2)
+        fusion = fusion_leg(world, rank, local, steps=max(20, args.steps), warmup=4)
         if fusion is not None and not args.no_cpu_baseline and world == 1:
             fusion["cpu_baseline"] = fusion_cpu_baseline()
 
