@@ -127,6 +127,29 @@ def test_clip_image_device_batch_consistency(vision, cuda):
     np.testing.assert_allclose(a[3:6], b, atol=1e-6)
 
 
+def test_batches_in_flight_bit_identical(vision, cuda):
+    """The bench's work-in-flight form (bench_clip_images): three encoder handles, each batch on
+    its own stream, enqueued from one thread without host syncs; every batch's embeddings equal
+    the serial call's bit for bit (same weights, independent workspaces)."""
+    import torch
+
+    from app.encoders import CLIP_VISION_B32, GpuEncoder
+
+    g = torch.Generator(device=cuda).manual_seed(9)
+    batches = [torch.randint(0, 256, (40 + 8 * i, 224, 224, 3), generator=g, dtype=torch.uint8, device=cuda)
+               for i in range(6)]
+    serial = [vision.embed_images(b).cpu() for b in batches]
+    encs = [GpuEncoder(CLIP_VISION_B32) for _ in range(3)]
+    streams = [torch.cuda.Stream(device=cuda) for _ in range(3)]
+    outs = [None] * len(batches)
+    for i, b in enumerate(batches):
+        with torch.cuda.stream(streams[i % 3]):
+            outs[i] = encs[i % 3].embed_images(b)
+    torch.cuda.synchronize()
+    for i in range(len(batches)):
+        assert torch.equal(outs[i].cpu(), serial[i]), i
+
+
 def test_clip_text_golden(cuda):
     from app.encoders import CLIP_TEXT_B32, GpuEncoder
 
