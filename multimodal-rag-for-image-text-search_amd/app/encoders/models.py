@@ -92,11 +92,52 @@ class MiniLMSentenceModel:
         return out if convert_to_tensor else out.cpu().numpy()
 
 
+class _HandlePool:
+    """Encoder handles of one model for concurrent callers: a call takes a free handle (a new one,
+    up to `limit`, when all are busy; else it waits), so requests from several threads run their
+    forwards at once on separate workspaces and streams instead of queueing on one handle's lock
+    (three image batches in flight: +23 % throughput, notes/work_in_flight.md). Every handle
+    holds the same weights, so a request's result does not depend on the handle it got.
+    env MRAG_ENCODER_HANDLES (default 3; 1 = one handle, the round-1 behaviour)."""
+
+    def __init__(self, make):
+        import threading
+
+        self._make = make
+        self._limit = max(1, int(os.environ.get("MRAG_ENCODER_HANDLES", "3")))
+        self._all = []
+        self._free = []
+        self._cv = threading.Condition()
+
+    def first(self):
+        with self._cv:
+            if not self._all:
+                h = self._make()
+                self._all.append(h)
+                self._free.append(h)
+            return self._all[0]
+
+    def acquire(self):
+        with self._cv:
+            while not self._free and len(self._all) >= self._limit:
+                self._cv.wait()
+            if self._free:
+                return self._free.pop()
+            h = self._make()
+            self._all.append(h)
+            return h
+
+    def release(self, h):
+        with self._cv:
+            self._free.append(h)
+            self._cv.notify()
+
+
 class ClipModel:
     def __init__(self, name: Optional[str] = None, device: Optional[int] = None):
         self.dir = _model_dir(name)  # raises here, as CLIPModel.from_pretrained would
         self.device = _device_index() if device is None else device
-        self._vision = None
+        self._vision_pool = _HandlePool(lambda: load_encoder(CLIP_VISION_B32, self.dir, device=self.device))
         self._text = None
 
     def to(self, device):
@@ -114,9 +155,7 @@ class ClipModel:
 
     @property
     def vision(self):
-        if self._vision is None:
-            self._vision = load_encoder(CLIP_VISION_B32, self.dir, device=self.device)
-        return self._vision
+        return self._vision_pool.first()
 
     @property
     def text(self):
@@ -130,7 +169,12 @@ class ClipModel:
         if images_u8 is None:
             raise TypeError("the GPU image tower takes u8 224x224 images (images_u8=), as produced by ClipProcessor")
         x = images_u8 if isinstance(images_u8, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(images_u8))
-        return self.vision.embed_images(x.to(f"cuda:{self.device}"), normalize=False)
+        x = x.to(f"cuda:{self.device}")
+        h = self._vision_pool.acquire()  # a handle reused on another stream waits for its last call
+        try:
+            return h.embed_images(x, normalize=False)
+        finally:
+            self._vision_pool.release(h)
 
     def get_text_features(self, input_ids=None, attention_mask=None, **kw):
         import torch

@@ -226,3 +226,39 @@ print("ok")
     got = store.search_text("alice", X[0], 2)
     assert {g["chunk_id"] for g in got} == {"c0", "c8"}
     ls._REGISTRY.clear()
+
+
+def test_clip_model_concurrent_requests(cuda):
+    """The drop-in ClipModel serves concurrent get_image_features calls on a pool of encoder
+    handles (same weights): results from four threads equal the serial calls bit for bit."""
+    import threading
+
+    import torch
+
+    from app.encoders.models import ClipModel
+
+    from app.settings import settings
+
+    m = ClipModel(settings.models.clip)
+    g = torch.Generator(device=cuda).manual_seed(4)
+    batches = [torch.randint(0, 256, (24 + 8 * i, 224, 224, 3), generator=g, dtype=torch.uint8, device=cuda)
+               for i in range(8)]
+    serial = [m.get_image_features(images_u8=b).cpu() for b in batches]
+    outs = [None] * len(batches)
+    errs = []
+
+    def work(i):
+        try:
+            outs[i] = m.get_image_features(images_u8=batches[i]).cpu()
+        except Exception as e:  # surfaced below
+            errs.append(e)
+
+    th = [threading.Thread(target=work, args=(i,)) for i in range(len(batches))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+    assert not errs, errs
+    for i in range(len(batches)):
+        assert torch.equal(outs[i], serial[i]), i
+    assert 1 <= len(m._vision_pool._all) <= 3
