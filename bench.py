@@ -76,6 +76,45 @@ def _barrier(world: int):
         dist.barrier()
 
 
+def _cgroup_cpus():
+    """CPUs the cgroup quota grants this process (cgroup v2 cpu.max), or None without a quota."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota == "max":
+            return None
+        return max(1, -(-int(quota) // int(period)))
+    except Exception:
+        return None
+
+
+def _usable_cores() -> int:
+    """Host cores the CPU baselines use: every core in this process's affinity mask, capped by
+    the cgroup CPU quota when one is set (the GPU box's affinity lists the whole node while the
+    job's share is a fraction of it; more threads than the quota only time-slice)."""
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except Exception:
+        cores = os.cpu_count() or 1
+    q = _cgroup_cpus()
+    return min(cores, q) if q else cores
+
+
+def _use_all_cores():
+    """torch intra-op threads and the BLAS pool at _usable_cores() for a CPU baseline."""
+    import torch
+
+    n = _usable_cores()
+    torch.set_num_threads(n)
+    try:
+        from threadpoolctl import threadpool_limits
+
+        threadpool_limits(limits=n, user_api="blas")
+    except Exception:
+        pass
+    return n
+
+
 def _host_info():
     """Host cores this process may use, torch's intra-op threads, the BLAS numpy links."""
     import torch
@@ -94,8 +133,8 @@ def _host_info():
                 break
     except Exception:
         pass
-    return {"affinity_cores": cores, "torch_threads": int(torch.get_num_threads()), "blas": blas,
-            "blas_threads": blas_threads}
+    return {"affinity_cores": cores, "cgroup_cpus": _cgroup_cpus(), "usable_cores": _usable_cores(),
+            "torch_threads": int(torch.get_num_threads()), "blas": blas, "blas_threads": blas_threads}
 
 
 def _median_rate(fn, units: int, reps: int = 5):
@@ -118,6 +157,8 @@ def cpu_baseline(seconds_budget: float = 20.0):
     threaded selection). The exact f64 oracle stays the checker only (tests)."""
     import numpy as np
     import torch
+
+    _use_all_cores()
 
     rng = np.random.default_rng(0)
     x = rng.standard_normal((ROWS_PER_GPU, DIM), dtype=np.float32)
@@ -166,6 +207,8 @@ def clip_cpu_baseline(seconds_budget: float = 12.0):
     import numpy as np
     import torch
 
+    _use_all_cores()
+
     from oracle.models import clip_image_embeds, clip_model
 
     model = clip_model(0)
@@ -200,6 +243,78 @@ def clip_leg(steps: int, warmup: int):
     out = bench_clip_images(steps=steps, warmup=warmup)  # three batches in flight
     one = bench_clip_images(steps=steps, warmup=warmup, inflight=1)
     out["one_batch_in_flight"] = {"images_per_s": one["value"], "ms_per_batch": one["ms_per_batch"]}
+    return out
+
+
+def call_pattern_leg(index, q, reps: int = 200):
+    """The reference's own call pattern over the same 1M x 512 shard: retrieve_text /
+    retrieve_images issue ONE query per search (app/ml/retrieve.py:53,84 ->
+    app/storage/lancedb_store.py:103-123). Timed here, one GPU, beside `value` (never as it):
+
+    * ``device_q{1,8}``: FlatIndex.search of 1 / 8 device-resident queries on a stream (the scan
+      streams the corpus once per search: K7s, the 64-query scan instance), with the K7 launch
+      time from the in-library HIP events -> HBM GB/s of the corpus read (N * D * 2 bytes);
+    * ``host_q1``: numpy query in, numpy results out (PCIe both ways);
+    * ``dropin_search_image``: ``LanceDBStore.search_image(user_id, vec.tolist(), 10)`` through
+      the drop-in module on a 1M-row table (Python list in, formatted hit dicts out)."""
+    import numpy as np
+    import torch
+
+    out = {}
+    dev = q.device
+    stream = torch.cuda.Stream(device=dev)
+    for nq in (1, 8):
+        qq = q[:nq].contiguous()
+        with torch.cuda.stream(stream):
+            for _ in range(10):
+                index.search(qq, TOPK)
+            stream.synchronize()
+            index.profile(1)
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                index.search(qq, TOPK)
+            stream.synchronize()
+            dt = (time.perf_counter() - t0) / reps
+            scan_ms, n = index.profile(0)
+        scan_s = scan_ms / max(n, 1) / 1e3
+        gbs = ROWS_PER_GPU * DIM * 2 / scan_s / 1e9 if scan_s > 0 else 0.0
+        out[f"device_q{nq}"] = {"ms_per_search": round(dt * 1e3, 4), "queries_per_s": round(nq / dt, 1),
+                                "scan_ms": round(scan_s * 1e3, 4), "scan_hbm_gbs": round(gbs, 1),
+                                "scan_hbm_frac": round(gbs / HBM_PEAK_GBS, 4)}
+    qh = q[:1].cpu().numpy()
+    for _ in range(10):
+        index.search(qh, TOPK)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        index.search(qh, TOPK)
+    dt = (time.perf_counter() - t0) / reps
+    out["host_q1"] = {"ms_per_search": round(dt * 1e3, 4), "queries_per_s": round(1 / dt, 1)}
+
+    # the drop-in store over the same GPU index: one table of 1M rows of user "u0"
+    os.environ["MRAG_STORE_PERSIST"] = "0"
+    import tempfile
+
+    from app.storage.lancedb_store import LanceDBStore
+
+    store = LanceDBStore(tempfile.mkdtemp(prefix="mrag_bench_store_"))
+    t = store._image_table
+    t.index, t.dim = index, DIM
+    t.chunk_ids = [f"c{i}" for i in range(ROWS_PER_GPU)]
+    t.metas = ["{}"] * ROWS_PER_GPU
+    t.labels = {"u0": 0}
+    vec = q[0].cpu().numpy().tolist()
+    hits = store.search_image("u0", vec, TOPK)
+    for _ in range(10):
+        store.search_image("u0", vec, TOPK)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        store.search_image("u0", vec, TOPK)
+    dt = (time.perf_counter() - t0) / reps
+    out["dropin_search_image"] = {"ms_per_call": round(dt * 1e3, 4), "calls_per_s": round(1 / dt, 1),
+                                  "hits": len(hits)}
+    t.index = None  # the bench owns the index
+    out["note"] = ("one query per search, the reference's call pattern (retrieve_text / retrieve_images); "
+                   "scan_hbm_gbs = 1M x 512 fp16 corpus bytes / K7 launch time (HIP events)")
     return out
 
 
@@ -246,6 +361,8 @@ def fusion_cpu_baseline(seconds_budget: float = 20.0):
     query. Median of 5 timed batches."""
     import numpy as np
     import torch
+
+    _use_all_cores()
 
     from oracle.fusion import fuse_results
     from oracle.models import clip_text_embeds, minilm_embeds
@@ -449,6 +566,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-clip", action="store_true")
     ap.add_argument("--no-fusion", action="store_true")
+    ap.add_argument("--no-call-pattern", action="store_true")
     ap.add_argument("--knn-streams", type=int, default=2,
                     help="kNN searches in flight (host threads / streams); 1 = one at a time")
     args = ap.parse_args()
@@ -550,6 +668,10 @@ def main():
         host_path = {"queries_per_s": round(NQ * n_host / dt_host, 1), "ms_per_search": round(dt_host / n_host * 1e3, 4),
                      "note": "numpy queries in / numpy results out (PCIe-inclusive, host buffers); not `value`"}
 
+    call_pattern = None
+    if world == 1 and not args.no_call_pattern:
+        call_pattern = call_pattern_leg(index, q)
+
     fusion = None
     if not args.no_fusion:  # config 5 (all ranks take part: sharded corpora + all-gathers)
         del sharded
@@ -608,6 +730,8 @@ def main():
                 out["clip"] = clip
         if host_path is not None:
             out["host_buffer_path"] = host_path
+        if call_pattern is not None:
+            out["call_pattern"] = call_pattern
         if fusion is not None:
             out["fusion"] = fusion
         if not args.no_cpu_baseline and world == 1:

@@ -18,10 +18,10 @@ from typing import Optional, Sequence, Tuple
 
 import numpy as np
 
-from app.encoders import CLIP_TEXT_B32, CLIP_VISION_B32, MINILM_L6, load_encoder
+from app.encoders import CLIP_TEXT_B32, CLIP_VISION_B32, MINILM_L6, GpuEncoder, load_encoder
 from app.encoders.preprocess import load_batch, load_batch_device
 from app.encoders.tokenize import ClipTokenizer, WordPieceTokenizer
-from app.encoders.weights import resolve_model_dir, synthetic_allowed, SYNTHETIC_ENV
+from app.encoders.weights import encoder_weights, resolve_model_dir, synth_state_dict, synthetic_allowed, SYNTHETIC_ENV
 
 
 def _device_index() -> int:
@@ -65,8 +65,13 @@ class MiniLMSentenceModel:
     def __init__(self, name: Optional[str] = None, device: Optional[int] = None):
         d = _model_dir(name, _WORDPIECE_FILES)
         self.device = _device_index() if device is None else device
-        self.enc = load_encoder(MINILM_L6, d, device=self.device)
+        self._pool = _HandlePool(_handle_maker(MINILM_L6, d, self.device))
+        self._pool.first()  # load now, as SentenceTransformer(name) does
         self.tokenizer = WordPieceTokenizer(d, max_len=256)
+
+    @property
+    def enc(self):
+        return self._pool.first()
 
     def to(self, device):
         return self
@@ -83,13 +88,43 @@ class MiniLMSentenceModel:
         # GPU batch is sized for throughput (>= the caller's batch_size)
         order = np.argsort([-len(s) for s in sentences], kind="stable")
         gb = max(int(batch_size), 256)
-        for s0 in range(0, len(order), gb):
-            idx = order[s0:s0 + gb]
-            ids, mask = self.tokenizer([sentences[i] for i in idx])
-            emb = self.enc.embed_tokens(torch.from_numpy(ids).to(out.device), torch.from_numpy(mask).to(out.device),
-                                        normalize=True)
-            out[torch.from_numpy(idx).to(out.device)] = emb
-        return out if convert_to_tensor else out.cpu().numpy()
+        h = self._pool.acquire()  # concurrent callers run on their own handles / streams
+        try:
+            for s0 in range(0, len(order), gb):
+                idx = order[s0:s0 + gb]
+                ids, mask = self.tokenizer([sentences[i] for i in idx])
+                emb = h.embed_tokens(torch.from_numpy(ids).to(out.device), torch.from_numpy(mask).to(out.device),
+                                     normalize=True)
+                out[torch.from_numpy(idx).to(out.device)] = emb
+            res = out if convert_to_tensor else out.cpu().numpy()
+        finally:
+            self._pool.release(h)
+        return res
+
+
+def _handle_maker(cfg, model_dir, device):
+    """Builder of identical encoder handles for a _HandlePool: the checkpoint (or the synthetic
+    state dict) is read once and shared by every handle of the pool; the pool drops it once it
+    holds all its handles."""
+    import threading
+
+    lock = threading.Lock()
+    cache = {}
+
+    def make():
+        with lock:
+            if "sd" not in cache:
+                sd, _ = encoder_weights(cfg, model_dir)
+                cache["sd"] = sd if sd is not None else dict(synth_state_dict(cfg, 0))
+            sd = cache["sd"]
+        return GpuEncoder(cfg, device=device, state_dict=sd)
+
+    def done():
+        with lock:
+            cache.clear()
+
+    make.done = done
+    return make
 
 
 class _HandlePool:
@@ -97,7 +132,9 @@ class _HandlePool:
     up to `limit`, when all are busy; else it waits), so requests from several threads run their
     forwards at once on separate workspaces and streams instead of queueing on one handle's lock
     (three image batches in flight: +23 % throughput, notes/work_in_flight.md). Every handle
-    holds the same weights, so a request's result does not depend on the handle it got.
+    holds the same weights, so a request's result does not depend on the handle it got. A new
+    handle is built outside the pool's lock (a slot is reserved first), so releases and other
+    acquirers never wait for a weight upload.
     env MRAG_ENCODER_HANDLES (default 3; 1 = one handle, the round-1 behaviour)."""
 
     def __init__(self, make):
@@ -107,38 +144,60 @@ class _HandlePool:
         self._limit = max(1, int(os.environ.get("MRAG_ENCODER_HANDLES", "3")))
         self._all = []
         self._free = []
+        self._pending = 0  # slots reserved by handles being built
         self._cv = threading.Condition()
+
+    def _build(self, free_it: bool):
+        try:
+            h = self._make()
+        except BaseException:
+            with self._cv:
+                self._pending -= 1
+                self._cv.notify_all()
+            raise
+        with self._cv:
+            self._pending -= 1
+            self._all.append(h)
+            if free_it:
+                self._free.append(h)
+            full = len(self._all) >= self._limit
+            self._cv.notify_all()
+        if full and hasattr(self._make, "done"):
+            self._make.done()  # every handle built: the shared host weights are no longer needed
+        return h
 
     def first(self):
         with self._cv:
-            if not self._all:
-                h = self._make()
-                self._all.append(h)
-                self._free.append(h)
+            while not self._all and self._pending:
+                self._cv.wait()
+            if self._all:
+                return self._all[0]
+            self._pending += 1
+        self._build(free_it=True)
+        with self._cv:
             return self._all[0]
 
     def acquire(self):
         with self._cv:
-            while not self._free and len(self._all) >= self._limit:
+            while not self._free and len(self._all) + self._pending >= self._limit:
                 self._cv.wait()
             if self._free:
                 return self._free.pop()
-            h = self._make()
-            self._all.append(h)
-            return h
+            self._pending += 1
+        return self._build(free_it=False)
 
     def release(self, h):
         with self._cv:
             self._free.append(h)
-            self._cv.notify()
+            self._cv.notify_all()
 
 
 class ClipModel:
     def __init__(self, name: Optional[str] = None, device: Optional[int] = None):
         self.dir = _model_dir(name)  # raises here, as CLIPModel.from_pretrained would
         self.device = _device_index() if device is None else device
-        self._vision_pool = _HandlePool(lambda: load_encoder(CLIP_VISION_B32, self.dir, device=self.device))
-        self._text = None
+        self._vision_pool = _HandlePool(_handle_maker(CLIP_VISION_B32, self.dir, self.device))
+        self._text_pool = None
 
     def to(self, device):
         return self
@@ -157,11 +216,14 @@ class ClipModel:
     def vision(self):
         return self._vision_pool.first()
 
+    def _texts(self):
+        if self._text_pool is None:
+            self._text_pool = _HandlePool(_handle_maker(self._text_cfg(), self.dir, self.device))
+        return self._text_pool
+
     @property
     def text(self):
-        if self._text is None:
-            self._text = load_encoder(self._text_cfg(), self.dir, device=self.device)
-        return self._text
+        return self._texts().first()
 
     def get_image_features(self, images_u8=None, pixel_values=None, **kw):
         import torch
@@ -185,7 +247,12 @@ class ClipModel:
         if attention_mask is not None:
             m = attention_mask if isinstance(attention_mask, torch.Tensor) else torch.from_numpy(np.asarray(attention_mask))
             m = m.to(dev)
-        return self.text.embed_tokens(ids.to(dev), m, normalize=False)
+        pool = self._texts()
+        h = pool.acquire()  # concurrent query encodes run on their own handles / streams
+        try:
+            return h.embed_tokens(ids.to(dev), m, normalize=False)
+        finally:
+            pool.release(h)
 
 
 class ClipProcessor:

@@ -88,8 +88,14 @@ def retrieve_batch(user_id: str, queries: Sequence[str], top_k_text: Optional[in
     try:
         text_vecs = r.embed_text_batch(qs)
         th = search_batch("text", user_id, text_vecs, tk)
-    finally:
-        ih = fut.result()  # re-raises the image branch's error, after the text branch is done
+    except BaseException as text_err:
+        # the text branch's error is the one raised; wait for the image branch first (it shares
+        # the GPU and the store) and chain its error, if any, instead of replacing this one
+        img_err = fut.exception()
+        if img_err is not None and text_err.__cause__ is None:
+            raise text_err from img_err
+        raise
+    ih = fut.result()  # re-raises the image branch's error
     _, meta = _store()
     out = []
     for i in range(len(qs)):

@@ -48,6 +48,30 @@ struct DeviceGuard {
     if (!(cond)) return mrag::fail(MRAG_ERR_ARG, __VA_ARGS__); \
   } while (0)
 
+namespace mrag {
+
+// Device-pointer inputs with stream == NULL run on a handle's own non-blocking stream, which
+// does not wait for the null stream by itself: order it after everything already queued there
+// (torch's default stream), so inputs produced by earlier kernels are complete when read.
+inline int wait_null_stream(hipEvent_t ev, hipStream_t s) {
+  MRAG_HIP(hipEventRecord(ev, nullptr));
+  MRAG_HIP(hipStreamWaitEvent(s, ev, 0));
+  return MRAG_OK;
+}
+
+// Drains a stream on scope exit unless disarmed: an error return after the first launch must not
+// hand buffers that queued kernels still use back to a pool (or drop the lock guarding them).
+struct StreamDrain {
+  hipStream_t s;
+  bool armed = true;
+  explicit StreamDrain(hipStream_t st) : s(st) {}
+  ~StreamDrain() {
+    if (armed) (void)hipStreamSynchronize(s);
+  }
+};
+
+}  // namespace mrag
+
 // ---------------------------------------------------------------------------
 // Device-side helpers
 // ---------------------------------------------------------------------------

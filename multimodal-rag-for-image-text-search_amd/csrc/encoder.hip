@@ -77,6 +77,7 @@ struct mrag_encoder {
   // drains it.
   hipEvent_t done = nullptr;
   hipStream_t last_stream = nullptr;
+  hipEvent_t null_ev = nullptr;  // device inputs on the NULL stream: the call waits for it
 };
 
 namespace {
@@ -227,11 +228,17 @@ int ensure_workspace(mrag_encoder* e, int B, int T) {
   if (e->last_stream) MRAG_HIP(hipEventSynchronize(e->done));  // in-flight work still reads the old buffers
   const auto& c = e->cfg;
   const int64_t D = c.hidden, I = c.intermediate;
-  if (B > e->ws_batch) {  // pooled rows of the last CLIP layer (clip_layer_pooled)
-    if (int rc = buf_ensure(e->XG, (size_t)B * D * 4)) return rc;
+  // per-sequence buffers grow with B, per-token ones with B * T: either can grow alone (the
+  // tokenisers pad to the longest sequence of a batch, so B can grow while B * T does not)
+  if (B > e->ws_batch) {
+    if (int rc = buf_ensure(e->XG, (size_t)B * D * 4)) return rc;  // pooled rows of the last CLIP layer
     if (int rc = buf_ensure(e->AG, (size_t)B * D * 2)) return rc;
     if (int rc = buf_ensure(e->HG, (size_t)B * D * 2)) return rc;
     if (int rc = buf_ensure(e->FG, (size_t)B * I * 2)) return rc;
+    if (int rc = buf_ensure(e->ROWS, (size_t)B * 4 + 256)) return rc;
+    if (int rc = buf_ensure(e->POOL16, (size_t)B * D * 2)) return rc;
+    if (c.kind == MRAG_ENC_BERT_PAIR)
+      if (int rc = buf_ensure(e->POOL32, (size_t)B * D * 4)) return rc;
     e->ws_batch = B;
   }
   if (tokens <= e->ws_tokens) return MRAG_OK;
@@ -245,10 +252,6 @@ int ensure_workspace(mrag_encoder* e, int B, int T) {
   if (c.kind == MRAG_ENC_CLIP_VISION) {
     if (int rc = buf_ensure(e->PATCH, tokens * D * 4)) return rc;
   }
-  if (int rc = buf_ensure(e->ROWS, (size_t)B * 4 + 256)) return rc;
-  if (int rc = buf_ensure(e->POOL16, (size_t)B * D * 2)) return rc;
-  if (c.kind == MRAG_ENC_BERT_PAIR)
-    if (int rc = buf_ensure(e->POOL32, (size_t)B * D * 4)) return rc;
   e->ws_tokens = tokens;
   return MRAG_OK;
 }
@@ -423,6 +426,7 @@ int mrag_encoder_create(const mrag_encoder_config* cfg, int32_t device, mrag_enc
   e->expected = expected_names(c);
   hipError_t err = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
   if (err == hipSuccess) err = hipEventCreateWithFlags(&e->done, hipEventDisableTiming);
+  if (err == hipSuccess) err = hipEventCreateWithFlags(&e->null_ev, hipEventDisableTiming);
   if (err != hipSuccess) {
     delete e;
     return mrag::fail(MRAG_ERR_HIP, "stream: %s", hipGetErrorString(err));
@@ -438,6 +442,7 @@ int mrag_encoder_destroy(mrag_encoder* e) {
     (void)hipStreamSynchronize(e->stream);
     if (e->last_stream) (void)hipEventSynchronize(e->done);
     if (e->done) (void)hipEventDestroy(e->done);
+    if (e->null_ev) (void)hipEventDestroy(e->null_ev);
     for (auto& L : e->layers)
       for (Buf* b : {&L.wqkv, &L.bqkv, &L.wo, &L.bo, &L.w1, &L.b1, &L.w2, &L.b2, &L.ln1g, &L.ln1b, &L.ln2g, &L.ln2b})
         buf_free(*b);
@@ -549,9 +554,12 @@ int mrag_encoder_missing(const mrag_encoder* e, int64_t* count) {
   return MRAG_OK;
 }
 
-// Start of a forward on stream s: order it after the previous call if that ran elsewhere.
-int begin_call(mrag_encoder* e, hipStream_t s) {
+// Start of a forward on stream s: order it after the previous call if that ran elsewhere, and
+// after the null stream's work when device inputs come without a caller stream.
+int begin_call(mrag_encoder* e, hipStream_t s, int32_t ptr_kind, void* stream_arg) {
   if (e->last_stream && e->last_stream != s) MRAG_HIP(hipStreamWaitEvent(s, e->done, 0));
+  if (ptr_kind == MRAG_PTR_DEVICE && stream_arg == nullptr)
+    if (int rc = mrag::wait_null_stream(e->null_ev, s)) return rc;
   return MRAG_OK;
 }
 
@@ -577,7 +585,8 @@ int mrag_encoder_embed_images(mrag_encoder* e, const uint8_t* images, int32_t ba
   if (batch == 0) return MRAG_OK;
   MRAG_REQUIRE(images && out, "NULL images/out");
   hipStream_t s = stream_arg ? (hipStream_t)stream_arg : e->stream;
-  if (int rc = begin_call(e, s)) return rc;
+  if (int rc = begin_call(e, s, ptr_kind, stream_arg)) return rc;
+  mrag::StreamDrain drain(s);  // an error return after a launch drains s (workspace reuse)
   const auto& c = e->cfg;
   const int S = c.image_size, P = c.patch_size, G = S / P, T = G * G + 1, D = c.hidden, B = batch;
   const int Kp = 3 * P * P;
@@ -616,6 +625,7 @@ int mrag_encoder_embed_images(mrag_encoder* e, const uint8_t* images, int32_t ba
     if (int rc = mrag_l2norm_rows(dst, dst, B, c.proj_dim, s)) return rc;
   if (ptr_kind == MRAG_PTR_HOST)
     MRAG_HIP(hipMemcpyAsync(out, dst, (size_t)B * c.proj_dim * 4, hipMemcpyDeviceToHost, s));
+  drain.armed = false;
   return end_call(e, s, ptr_kind, stream_arg);
 }
 
@@ -633,7 +643,8 @@ int mrag_encoder_embed_tokens(mrag_encoder* e, const int32_t* ids, const int32_t
   if (batch == 0) return MRAG_OK;
   MRAG_REQUIRE(ids && out, "NULL ids/out");
   hipStream_t s = stream_arg ? (hipStream_t)stream_arg : e->stream;
-  if (int rc = begin_call(e, s)) return rc;
+  if (int rc = begin_call(e, s, ptr_kind, stream_arg)) return rc;
+  mrag::StreamDrain drain(s);  // an error return after a launch drains s (workspace reuse)
   const auto& c = e->cfg;
   const int B = batch, T = seq, D = c.hidden;
   if (int rc = ensure_workspace(e, B, T)) return rc;
@@ -686,6 +697,7 @@ int mrag_encoder_embed_tokens(mrag_encoder* e, const int32_t* ids, const int32_t
   if (normalize)
     if (int rc = mrag_l2norm_rows(dst, dst, B, outD, s)) return rc;
   if (ptr_kind == MRAG_PTR_HOST) MRAG_HIP(hipMemcpyAsync(out, dst, (size_t)B * outD * 4, hipMemcpyDeviceToHost, s));
+  drain.armed = false;
   return end_call(e, s, ptr_kind, stream_arg);
 }
 
@@ -703,7 +715,8 @@ int mrag_encoder_score_pairs(mrag_encoder* e, const int32_t* ids, const int32_t*
   if (batch == 0) return MRAG_OK;
   MRAG_REQUIRE(ids && out, "NULL ids/out");
   hipStream_t s = stream_arg ? (hipStream_t)stream_arg : e->stream;
-  if (int rc = begin_call(e, s)) return rc;
+  if (int rc = begin_call(e, s, ptr_kind, stream_arg)) return rc;
+  mrag::StreamDrain drain(s);  // an error return after a launch drains s (workspace reuse)
   const auto& c = e->cfg;
   const int B = batch, T = seq, D = c.hidden, NL = c.proj_dim;
   if (int rc = ensure_workspace(e, B, T)) return rc;
@@ -755,6 +768,7 @@ int mrag_encoder_score_pairs(mrag_encoder* e, const int32_t* ids, const int32_t*
                                NL, s))
     return rc;
   if (ptr_kind == MRAG_PTR_HOST) MRAG_HIP(hipMemcpyAsync(out, dst, (size_t)B * NL * 4, hipMemcpyDeviceToHost, s));
+  drain.armed = false;
   return end_call(e, s, ptr_kind, stream_arg);
 }
 

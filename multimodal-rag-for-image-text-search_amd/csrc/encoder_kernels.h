@@ -19,11 +19,6 @@ struct GemmArgs {
   const float* bias;  // [N] or null
   void* C;            // [M][ldc] f16 or f32 per epilogue
   int M, N, K, lda, ldw, ldc;
-  // K3d stream-K workspace (set by the launcher, null otherwise): per workgroup two 256 KiB
-  // partial-accumulator slots, and one arrival counter per output tile (zero between launches)
-  float* sk_part;
-  int* sk_cnt;
-  int k3_remap;  // K3: XCD-contiguous tile order (set by the launcher)
 };
 
 struct LayerNormArgs {
@@ -49,8 +44,6 @@ int launch_gemm(const GemmArgs& g, int epi, hipStream_t s);
 int launch_layernorm(const LayerNormArgs& a, hipStream_t s);
 int launch_attention(const AttentionArgs& a, int dh, hipStream_t s);
 int launch_vit_im2col(const uint8_t* img, _Float16* out, int B, int S, int P, hipStream_t s);
-int launch_vit_assemble(const float* patch, const float* cls, const float* pos, float* X, int B, int T, int D,
-                        hipStream_t s);
 int launch_vit_embed_ln(const float* patch, const float* cls, const float* pos, const float* gamma, const float* beta,
                         float* X, int B, int T, int D, float eps, hipStream_t s);
 int launch_token_embed(const int32_t* ids, const float* tok, const float* pos, const float* type_tab,

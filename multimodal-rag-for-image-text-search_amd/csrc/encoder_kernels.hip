@@ -153,9 +153,8 @@ __global__ __launch_bounds__(GTHREADS) void gemm_nt_kernel(GemmArgs g) {
   const int tiles_n = g.N / GN;
   // consecutive tile ids walk N for a fixed M panel; blocks b, b + 8, ... (one XCD under the
   // round-robin dispatch) take consecutive tile ids (xcd_remap), so the tiles_n tiles of an A
-  // panel are fetched into ONE XCD's L2 instead of being dealt over tiles_n XCDs (speed only;
-  // env MRAG_K3_REMAP=0 keeps the plain order for A/B timing)
-  const int T = g.k3_remap ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+  // panel are fetched into ONE XCD's L2 instead of being dealt over tiles_n XCDs (speed only)
+  const int T = xcd_remap(blockIdx.x, gridDim.x);
   const int tm = T / tiles_n, tn = T - (T / tiles_n) * tiles_n;
   const int m0 = tm * GM, n0 = tn * GN;
   const int ksteps = g.K / GK;
@@ -267,12 +266,10 @@ constexpr int G8_THREADS = 512;
 constexpr int G8_BUF = 65536;      // one K-tile: two A and two B half-tile slots
 constexpr int G8_BIAS_MAX = 4096;  // bias floats staged in LDS
 
-// Tile geometry. CFG 0: 256 x 256 tiles (waves of 128 x 64). CFG 1: 128 x 384 tiles (waves of
-// 64 x 96) for N = 768 (out-proj, fc2 of ViT-B/32): 200 tiles instead of 150 on 256 CUs, one
-// round of 3/4-size tiles. Same per-element accumulation order and epilogue in both.
-template <int CFG>
+// Tile geometry: 256 x 256 tiles, waves of 128 x 64 (a 128 x 384 geometry for N = 768 and a
+// stream-K variant were measured slower: notes/gemm_experiments.md).
 struct G8Geom {
-  static constexpr int BM = CFG == 0 ? 256 : 128, BN = CFG == 0 ? 256 : 384;
+  static constexpr int BM = 256, BN = 256;
   static constexpr int WM = BM / 2, WN = BN / 4;  // wave tile (2 x 4 waves)
   static constexpr int HM = WM / 2, HN = WN / 2;  // one phase's quadrant
   static constexpr int NI = HM / 16, NJ = HN / 16;
@@ -281,14 +278,13 @@ struct G8Geom {
   static constexpr int slot_off(int sl) { return sl == 0 ? 0 : sl == 1 ? SA : sl == 2 ? SA + SB : SA + 2 * SB; }
   static constexpr int pieces(int sl) { return (sl == 0 || sl == 3) ? PA : PB; }
   static_assert(2 * SA + 2 * SB == G8_BUF, "a K-tile is 64 KiB");
-  static_assert(NJ == 2 || NJ == 3, "column permutation below");
+  static_assert(NJ == 2, "column permutation below");
 };
 // tile column (within a wave-column half) of B LDS row jj: lane group f of the 16 x 16 MFMA
-// blocks owns consecutive columns — 8 for the block pair jb = 0, 1 (one 16-byte f16 store),
-// 4 for a third block jb = 2 (one 8-byte store)
+// block pair jb = 0, 1 owns 8 consecutive columns (one 16-byte f16 store)
 __device__ __forceinline__ int g8_colperm(int jj) {
   const int jb = jj >> 4, f = (jj >> 2) & 3, r = jj & 3;
-  return jb < 2 ? 8 * f + 4 * jb + r : 32 + 4 * f + r;
+  return 8 * f + 4 * jb + r;
 }
 
 #define MRAG_VMCNT_CASE(n) \
@@ -313,44 +309,20 @@ __device__ __forceinline__ void vmcnt_wait(int n) {  // n wave-uniform, 0..63
 }
 #undef MRAG_VMCNT_CASE
 
-// ABL (timing experiments only, wrong results): 1 = no LDS-DMA in the loop, 2 = no
-// fragment ds_reads in the loop, 3 = both, 4 = no ping-pong stagger, 5 = LDS-DMA from the
-// first two K-tiles only (L2-hot), 7 = no epilogue stores
-//
-// SK = 1: stream-K. The tiles of an XCD (the same contiguous range as above) are laid out as
-// one sequence of K-tile iterations (tile-major) and cut into nbx equal contiguous ranges, one
-// per workgroup of that XCD, so every CU gets the same number of MFMA K-steps however the tile
-// count divides by 256 (ViT fc2 / out-proj: 150 tiles; fc1: 600). A range is a list of
-// segments (tile, k-tiles [kb, ke)); even workgroups walk their range forward, odd ones
-// backward, so the two pieces of a tile cut between workgroups s and s + 1 are computed at the
-// same time (both at the start or both at the end of their ranges). A piece of a cut tile
-// stores its raw accumulators to its slot (`sc1` 16-byte stores, each wave drains them, a
-// barrier), one lane adds to the tile's arrival counter (agent-scope atomic), and the
-// workgroup whose add comes last sums every piece IN K ORDER (p0 + p1 (+ p2), own piece from
-// registers, the others by `sc1` loads), resets the counter and runs the normal epilogue:
-// no workgroup ever waits for another (MI355X_MICROARCH.md, hand-off table row 1). The sum
-// order depends only on the cut points, i.e. on (M, N, K, grid): a launch is deterministic,
-// but a row's last bits can differ between batch sizes that cut differently (the launcher
-// uses SK only from M >= 8192 rows, so smaller batches keep the one-accumulator order).
-constexpr int SK_SLOT_BYTES = 256 * 256 * 4;  // one CFG-0 tile of f32 accumulators
-
-template <int EPI, int ABL = 0, int CFG = 0, int SK = 0>
+template <int EPI>
 __global__ __launch_bounds__(G8_THREADS) void gemm_8p_kernel(GemmArgs g) {
-  using GG = G8Geom<CFG>;
+  using GG = G8Geom;
   constexpr int BM = GG::BM, BN = GG::BN, WM = GG::WM, WN = GG::WN, HM = GG::HM, HN = GG::HN;
   constexpr int NI = GG::NI, NJ = GG::NJ, PA = GG::PA, PB = GG::PB;
-  static_assert(SK == 0 || (CFG == 0 && ABL == 0), "stream-K: 256 x 256 tiles only");
-  constexpr int BIAS_BYTES = ABL == 8 ? 16 : G8_BIAS_MAX * 4;
-  __shared__ __attribute__((aligned(16))) char smem[2 * G8_BUF + BIAS_BYTES + 16];
+  __shared__ __attribute__((aligned(16))) char smem[2 * G8_BUF + G8_BIAS_MAX * 4];
   float* sbias = (float*)(smem + 2 * G8_BUF);
-  int* sflag = (int*)(smem + 2 * G8_BUF + BIAS_BYTES);
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wr = w >> 2, wc = w & 3;
   const int fr = lane & 15, fq = lane >> 4;
   const uint32_t lds_base = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)((AS3 char*)smem));
 
-  // this workgroup's tiles: lo + s + k * nbx, k = 0 .. my_n - 1 (SK: see above)
+  // this workgroup's tiles: lo + s + k * nbx, k = 0 .. my_n - 1
   const int tiles_n = g.N / BN;
   const int ntiles = ((g.M + BM - 1) / BM) * tiles_n;
   const int xcd = blockIdx.x & 7, sidx = blockIdx.x >> 3;
@@ -360,35 +332,20 @@ __global__ __launch_bounds__(G8_THREADS) void gemm_8p_kernel(GemmArgs g) {
   const int cnt = q8 + (xcd < r8 ? 1 : 0);
   const int my_n = sidx < cnt ? (cnt - sidx + nbx - 1) / nbx : 0;
   const int ktiles = g.K / GK;
-  const int64_t Ix = (int64_t)cnt * ktiles;  // SK: K-tile iterations of this XCD
-  auto range_lo = [&](int s) { return (int64_t)s * Ix / nbx; };
-  const int64_t it0 = SK ? range_lo(sidx) : 0, it1 = SK ? range_lo(sidx + 1) : 0;
-  const int t_first = SK ? (int)(it0 / ktiles) : 0, t_last = SK ? (int)((it1 - 1) / ktiles) : 0;
-  const bool fwd = (sidx & 1) == 0;
-  const int nseg = SK ? (it1 > it0 ? t_last - t_first + 1 : 0) : my_n;
-  if (nseg == 0) return;  // whole workgroup, before any barrier
+  if (my_n == 0) return;  // whole workgroup, before any barrier
   // segment i of this workgroup: tile T, k-tiles [kb, ke)
   auto seg = [&](int i, int& T, int& kb, int& ke) {
-    if constexpr (SK) {
-      const int t = fwd ? t_first + i : t_last - i;
-      const int64_t base = (int64_t)t * ktiles;
-      kb = (int)(it0 > base ? it0 - base : 0);
-      ke = (int)(it1 - base < ktiles ? it1 - base : ktiles);
-      T = lo + t;
-    } else {
-      T = lo + sidx + i * nbx;
-      kb = 0;
-      ke = ktiles;
-    }
+    T = lo + sidx + i * nbx;
+    kb = 0;
+    ke = ktiles;
   };
+  const int nseg = my_n;
 
-  if constexpr (ABL != 8) {
-    for (int i = threadIdx.x; i < g.N; i += G8_THREADS) sbias[i] = g.bias ? g.bias[i] : 0.f;
-    __syncthreads();
-  }
+  for (int i = threadIdx.x; i < g.N; i += G8_THREADS) sbias[i] = g.bias ? g.bias[i] : 0.f;
+  __syncthreads();
 
   const int KH = 4 * ktiles;                                // half-tiles per tile
-  const int total = SK ? (int)(4 * (it1 - it0)) : my_n * KH;  // half-tiles of the whole stream
+  const int total = my_n * KH;  // half-tiles of the whole stream
 
   // staging: a slot with PX pieces per wave gets pieces PX w .. PX w + PX - 1 (8 LDS rows each)
   // from this wave; LDS row j = 8 (PX w + q) + (lane >> 3), chunk position lane & 7 holds
@@ -432,7 +389,7 @@ __global__ __launch_bounds__(G8_THREADS) void gemm_8p_kernel(GemmArgs g) {
   auto stage_slot = [&](auto SL) {
     constexpr int sl = decltype(SL)::value;
     constexpr int PX = GG::pieces(sl);
-    const int k0 = (ABL == 5 ? (ld_kt & 1) : ld_kt) * GK;
+    const int k0 = ld_kt * GK;
     const uint32_t dst = lds_base + (uint32_t)(ld_par * G8_BUF + GG::slot_off(sl)) + (uint32_t)(w * PX * 1024);
 #pragma unroll
     for (int q = 0; q < PX; ++q) {
@@ -472,8 +429,7 @@ __global__ __launch_bounds__(G8_THREADS) void gemm_8p_kernel(GemmArgs g) {
     for (int i = 0; i < NI; ++i)
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
-        if constexpr (ABL == 2 || ABL == 3) asm volatile("" : "+v"(fa[i][kk]));
-        else fa[i][kk] = *(const half8*)(slot + offA[i][kk]);
+        fa[i][kk] = *(const half8*)(slot + offA[i][kk]);
       }
   };
   auto readB = [&](const char* slot, half8 (&fb)[NJ][2]) {
@@ -481,8 +437,7 @@ __global__ __launch_bounds__(G8_THREADS) void gemm_8p_kernel(GemmArgs g) {
     for (int jb = 0; jb < NJ; ++jb)
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
-        if constexpr (ABL == 2 || ABL == 3) asm volatile("" : "+v"(fb[jb][kk]));
-        else fb[jb][kk] = *(const half8*)(slot + offB[jb][kk]);
+        fb[jb][kk] = *(const half8*)(slot + offB[jb][kk]);
       }
   };
   auto mfma_q = [&](f32x4 (&a)[NI][NJ], const half8 (&fb)[NJ][2]) {
@@ -516,7 +471,7 @@ __global__ __launch_bounds__(G8_THREADS) void gemm_8p_kernel(GemmArgs g) {
     // steady state: L[phi + 3 .. phi + 7] in flight = every slot once + slot sl again
     constexpr int YSTEADY = 2 * PA + 2 * PB + GG::pieces(sl);
     const bool full = phi + 7 < total;  // five younger half-tiles in flight
-    if (ABL != 1 && ABL != 3 && full) stage_slot(SL);
+    if (full) stage_slot(SL);
     const bool post = phi - st_phi <= 5;  // the last epilogue's stores are younger than L[phi + 2]
     if (__builtin_expect(full && !post, 1)) {
       vmcnt_wait(YSTEADY);
@@ -541,83 +496,8 @@ __global__ __launch_bounds__(G8_THREADS) void gemm_8p_kernel(GemmArgs g) {
     vmcnt_wait(younger(1, last));  // L[0], L[1] landed
     bar();
   }
-  // SK: the piece of local tile t held in `acc` (tile id T) is stored; returns true when this
-  // workgroup's piece arrived last and `acc` now holds the whole tile's sum (see above)
-  auto sk_piece = [&](int t, int T) -> bool {
-    if (wr == 0) bar();  // group 0 waits for group 1's last phase: both groups aligned
-    const __amdgpu_buffer_rsrc_t part = __builtin_amdgcn_make_buffer_rsrc(g.sk_part, 0, 0x7fffffff, 0x00020000);
-    const uint32_t tid16 = threadIdx.x * 16;
-    {
-      const uint32_t base = (uint32_t)(2 * blockIdx.x + (t == t_first ? 0 : 1)) * SK_SLOT_BYTES + tid16;
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int hh = 0; hh < 2; ++hh)
-#pragma unroll
-          for (int i = 0; i < NI; ++i)
-#pragma unroll
-            for (int jb = 0; jb < NJ; ++jb) {
-              const int r = ((h * 2 + hh) * NI + i) * NJ + jb;
-              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[h][hh][i][jb]), part,
-                                                     base + r * (G8_THREADS * 16), 0, 16 /* sc1 */);
-            }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's piece has left the CU
-    bar();
-    if (threadIdx.x == 0)
-      *sflag = __hip_atomic_fetch_add(g.sk_cnt + T, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
-    const int arrived = *sflag;
-    // the pieces of tile t: workgroups s_first .. s_last of this XCD, ascending s = ascending k
-    const int64_t tb = (int64_t)t * ktiles;
-    const int s_first = (int)(((tb + 1) * nbx - 1) / Ix), s_last = (int)(((tb + ktiles) * nbx - 1) / Ix);
-    int np = 0;
-    for (int s = s_first; s <= s_last; ++s) np += range_lo(s + 1) > range_lo(s) ? 1 : 0;
-    if (arrived != np - 1) return false;
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-      for (int hh = 0; hh < 2; ++hh) {
-        f32x4 v[NI][NJ];
-        bool first = true;
-        for (int s = s_first; s <= s_last; ++s) {
-          const int64_t a0 = range_lo(s), a1 = range_lo(s + 1);
-          if (a1 <= a0) continue;
-          if (s == sidx) {
-#pragma unroll
-            for (int i = 0; i < NI; ++i)
-#pragma unroll
-              for (int jb = 0; jb < NJ; ++jb) v[i][jb] = first ? acc[h][hh][i][jb] : v[i][jb] + acc[h][hh][i][jb];
-          } else {
-            const uint32_t base =
-                (uint32_t)(2 * (xcd + 8 * s) + (t == (int)(a0 / ktiles) ? 0 : 1)) * SK_SLOT_BYTES + tid16;
-            f32x4 p[NI][NJ];
-#pragma unroll
-            for (int i = 0; i < NI; ++i)
-#pragma unroll
-              for (int jb = 0; jb < NJ; ++jb) {
-                const int r = ((h * 2 + hh) * NI + i) * NJ + jb;
-                p[i][jb] = __builtin_bit_cast(
-                    f32x4, __builtin_amdgcn_raw_buffer_load_b128(part, base + r * (G8_THREADS * 16), 0, 16 /* sc1 */));
-              }
-#pragma unroll
-            for (int i = 0; i < NI; ++i)
-#pragma unroll
-              for (int jb = 0; jb < NJ; ++jb) v[i][jb] = first ? p[i][jb] : v[i][jb] + p[i][jb];
-          }
-          first = false;
-        }
-#pragma unroll
-        for (int i = 0; i < NI; ++i)
-#pragma unroll
-          for (int jb = 0; jb < NJ; ++jb) acc[h][hh][i][jb] = v[i][jb];
-      }
-    if (threadIdx.x == 0) __hip_atomic_store(g.sk_cnt + T, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return true;
-  };
-
   // waves 4..7 (one per SIMD beside a wave of 0..3) run one barrier behind waves 0..3
-  if (ABL != 4 && wr == 1) bar();
+  if (wr == 1) bar();
   int phi = 0;
   for (int sg = 0; sg < nseg; ++sg) {
     int T, kb, ke;
@@ -651,278 +531,33 @@ __global__ __launch_bounds__(G8_THREADS) void gemm_8p_kernel(GemmArgs g) {
     }
     st_phi = phi - 1;
     st_cnt = 0;
-    const bool split = SK && (kb != 0 || ke != ktiles);  // wave-uniform
-    if (split && !sk_piece(T - lo, T)) {
-      if (wr == 1) bar();  // restore the stagger (the workgroup's barrier counts stay equal)
-      continue;
-    }
 
     // epilogue: blocks (h, hh, i): row WM wr + HM h + 16 i + fr; columns WN wc + HN hh + 8 fq
-    // + (0..7) from the block pair jb = 0, 1 (one 16-byte f16 store, two for f32) and, for
-    // CFG 1, WN wc + HN hh + 32 + 4 fq + (0..3) from jb = 2 (one 8-byte f16 / 16-byte f32 store)
+    // + (0..7) from the block pair jb = 0, 1 (one 16-byte f16 store, two for f32)
     const int tm = T / tiles_n;
     const int m0 = tm * BM, n0 = (T - tm * tiles_n) * BN;
-    constexpr int SPB = ((EPI == EPI_F32_RESIDUAL || EPI == EPI_F32) ? 2 : 1) + (NJ == 3 ? 1 : 0);
+    constexpr int SPB = (EPI == EPI_F32_RESIDUAL || EPI == EPI_F32) ? 2 : 1;
 #pragma unroll
     for (int hh = 0; hh < 2; ++hh) {
-      const int nb = n0 + WN * wc + HN * hh;
-      const int n = nb + 8 * fq;
-      float bn[8], bn4[4];
+      const int n = n0 + WN * wc + HN * hh + 8 * fq;
+      float bn[8];
 #pragma unroll
-      for (int r = 0; r < 8; ++r) bn[r] = ABL == 8 ? 0.f : sbias[n + r];
-      if constexpr (NJ == 3) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) bn4[r] = ABL == 8 ? 0.f : sbias[nb + 32 + 4 * fq + r];
-      }
+      for (int r = 0; r < 8; ++r) bn[r] = sbias[n + r];
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
           const int mb = m0 + WM * wr + HM * h + 16 * i;  // wave-uniform block row
           const int m = mb + fr;
-          if constexpr (ABL == 7) {
-            asm volatile("" ::"v"(acc[h][hh][i][0]), "v"(acc[h][hh][i][1]), "v"(bn[0]));
-          } else if (mb < g.M) {  // uniform branch: a block with a valid row issues exactly
-            st_cnt += SPB;        // SPB vector stores (counted for the vmcnt bookkeeping)
-            if (m < g.M) {
-              gemm_store8<EPI>(g, m, n, acc[h][hh][i][0], acc[h][hh][i][1], bn);
-              if constexpr (NJ == 3) gemm_store4<EPI>(g, m, nb + 32 + 4 * fq, acc[h][hh][i][NJ - 1], bn4);
-            }
+          if (mb < g.M) {  // uniform branch: a block with a valid row issues exactly
+            st_cnt += SPB;  // SPB vector stores (counted for the vmcnt bookkeeping)
+            if (m < g.M) gemm_store8<EPI>(g, m, n, acc[h][hh][i][0], acc[h][hh][i][1], bn);
           }
         }
       }
     }
-    if (split && wr == 1) bar();  // restore the stagger after a cut tile's epilogue
   }
-  if (ABL != 4 && wr == 0) bar();  // same barrier count for both groups
-}
-
-// ---------------------------------------------------------------------------
-// K3e (M >= 1024, N % 256 == 0, K % 64 == 0): persistent, one workgroup per CU, 256 x 256
-// tiles, FOUR waves (2 x 2) of 128 x 128 — one wave per SIMD owning a quarter of the tile, so
-// every fragment a wave reads from LDS feeds 8 MFMAs (K3d's 128 x 64 waves: 4 or 8) and the
-// CU reads 128 KiB of fragments per 64 k instead of 192 KiB.
-//  * accumulators: 8 x 8 blocks of 16 x 16 per wave = 256 f32 per lane, AGPR-resident (asm
-//    MFMA operands);
-//  * LDS: two 64-KiB K-tiles (A: 256 rows x 128 B, then B: 256 rows x 128 B), 16-byte chunk c
-//    of row j at position c ^ ((j >> 1) & 7) (K3's conflict-free image). Rows of 128 B = 64 k
-//    keep every LDS-DMA request a whole 128-byte line (rows of 64 B doubled the L2 requests:
-//    notes/gemm_experiments.md);
-//  * a K-tile is consumed in two 32-deep halves with one fragment set per half (R0, R1: 64
-//    VGPRs each): half 0 of tile t runs on R0 while R1 is read from tile t; half 1 runs on R1
-//    while R0 is read from tile t + 1. Tile t is fully read once half 0 ends, so the single
-//    barrier per K-tile sits there: wait for K-tile t + 1 (own vmcnt), barrier, then the
-//    LDS-DMA of K-tile t + 2 into tile t's buffer is spread over half 1's MFMAs. The load stream
-//    runs across output tiles, so the epilogue overlaps the next tile's loads;
-//  * waves 0, 1 stage the A half of every K-tile, waves 2, 3 the B half: 16 one-KiB pieces (8
-//    rows of 128 B) per wave per K-tile through the SADDR form (lane part of the offset in a
-//    VGPR, the piece's row offset and k in SGPRs);
-//  * C^T blocks with the weight fragment as MFMA operand A and permuted weight rows, so a lane
-//    stores 8 consecutive columns (gemm_store8) — the same per-element accumulation order
-//    (32-deep chunks in ascending k, one accumulator) and epilogue as K3 / K3d, hence the same
-//    bits whichever kernel a batch size selects.
-constexpr int G4_THREADS = 256;
-constexpr int G4_SLOT = 65536;  // one 64-deep K-tile: A 32 KiB + B 32 KiB
-
-__device__ __forceinline__ void glds_x4_saddr(uint32_t voff, const void* sbase, uint32_t lds_addr) {
-  unsigned keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(voff), "s"(sbase), "s"(lds_addr)
-      : "memory");
-}
-
-// weight LDS row j (0..127 within a wave column) -> its tile column: lane group f of block pair
-// (2p, 2p + 1) owns the 8 consecutive columns 32 p + 8 f + 0..7. For j = 8 q + rr this splits
-// into a piece part (uniform) and a lane part.
-__device__ __forceinline__ constexpr int g4_colbase(int q) { return 32 * (q >> 2) + 16 * (q & 1) + 4 * ((q >> 1) & 1); }
-__device__ __forceinline__ constexpr int g4_collane(int rr) { return 8 * (rr >> 2) + (rr & 3); }
-
-template <int EPI>
-__global__ __launch_bounds__(G4_THREADS) void gemm_4w_kernel(GemmArgs g) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * G4_SLOT + G8_BIAS_MAX * 4];
-  float* sbias = (float*)(smem + 2 * G4_SLOT);
-  const int lane = threadIdx.x & 63;
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wr = w >> 1, wc = w & 1;
-  const int fr = lane & 15, fq = lane >> 4;
-  const uint32_t lds_base = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)((AS3 char*)smem));
-
-  // tiles: XCD x owns a contiguous range of tile ids (tm-major), round-robin over its workgroups
-  const int tiles_n = g.N / 256;
-  const int ntiles = ((g.M + 255) / 256) * tiles_n;
-  const int xcd = blockIdx.x & 7, sidx = blockIdx.x >> 3;
-  const int nbx = ((int)gridDim.x - xcd + 7) >> 3;
-  const int q8 = ntiles >> 3, r8 = ntiles & 7;
-  const int lo = xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8;
-  const int cnt = q8 + (xcd < r8 ? 1 : 0);
-  const int my_n = sidx < cnt ? (cnt - sidx + nbx - 1) / nbx : 0;
-  if (my_n == 0) return;  // whole workgroup, before any barrier
-
-  for (int i = threadIdx.x; i < g.N; i += G4_THREADS) sbias[i] = g.bias ? g.bias[i] : 0.f;
-
-  const int ktiles = g.K / 64;
-  const int total = my_n * ktiles;
-
-  // loader: piece q (0..15) of this wave = LDS rows 8 (16 (w & 1) + q) + rr, rr = lane >> 3, of
-  // the A half (waves 0, 1) or the B half (waves 2, 3); lane position lane & 7 holds source
-  // chunk (lane & 7) ^ ((row >> 1) & 7) (row & 15 = 8 (q & 1) + rr)
-  const bool loadsB = w >= 2;
-  const int rr = lane >> 3;
-  const uint32_t cb0 = (uint32_t)(((lane & 7) ^ (rr >> 1)) * 16);        // q even
-  const uint32_t cb1 = (uint32_t)(((lane & 7) ^ (4 + (rr >> 1))) * 16);  // q odd
-  const uint32_t ldb = (uint32_t)(loadsB ? g.ldw : g.lda) * 2u;          // row stride, bytes
-  const uint32_t vlaneB = (uint32_t)g4_collane(rr) * ldb;
-  const uint32_t lds_w = lds_base + (loadsB ? 32768u : 0u) + (uint32_t)(w & 1) * 16384u;
-  int ld_kt = 0, ld_T = lo + sidx;
-  int ld_m0 = 0, ld_n0 = 0;
-  auto load_tile_origin = [&]() {
-    const int tm = ld_T / tiles_n;
-    ld_m0 = tm * 256;
-    ld_n0 = (ld_T - tm * tiles_n) * 256;
-  };
-  load_tile_origin();
-  // piece q of K-tile L[t]: A rows ld_m0 + 128 (w & 1) + 8 q + rr (clamped to M - 1), B rows
-  // ld_n0 + 128 (w & 1) + g4_colbase(q) + g4_collane(rr)
-  auto issue_piece = [&](int t, int q) {
-    const uint32_t dst = lds_w + (uint32_t)(t & 1) * G4_SLOT + (uint32_t)q * 1024u;
-    const uint32_t cb = (q & 1) ? cb1 : cb0;
-    if (loadsB) {
-      const char* sb = (const char*)(g.W + (size_t)(ld_n0 + 128 * (w & 1) + g4_colbase(q)) * g.ldw + ld_kt * 64);
-      glds_x4_saddr(vlaneB + cb, sb, dst);
-    } else {
-      // rows past M re-read row M - 1: base row and lane row both clamped, so 0 <= row < M
-      const int rbase = min(ld_m0 + 128 * (w & 1) + 8 * q, g.M - 1);
-      const char* sb = (const char*)(g.A + (size_t)rbase * g.lda + ld_kt * 64);
-      const uint32_t row = (uint32_t)min(rr, g.M - 1 - rbase);
-      glds_x4_saddr(row * ldb + cb, sb, dst);
-    }
-  };
-  auto advance_loader = [&]() {
-    if (++ld_kt == ktiles) {
-      ld_kt = 0;
-      ld_T += nbx;
-      if (ld_T < ntiles) load_tile_origin();
-    }
-  };
-
-  // fragments: activation block i -> LDS A row 128 wr + 16 i + fr, weight block jb -> LDS B row
-  // 128 wc + 16 jb + fr; half kk reads chunk 4 kk + fq; blocks 2 KiB apart
-  int offA[2], offB[2];
-#pragma unroll
-  for (int kk = 0; kk < 2; ++kk) {
-    offA[kk] = swz_off(128 * wr + fr, 4 * kk + fq);
-    offB[kk] = 32768 + swz_off(128 * wc + fr, 4 * kk + fq);
-  }
-  half8 fa[2][8], fb[2][8];  // [half][block]
-
-  f32x4 acc[8][8];  // [activation block i][weight block jb], AGPR-resident (asm MFMA operand)
-  constexpr int SPB = (EPI == EPI_F32_RESIDUAL || EPI == EPI_F32) ? 2 : 1;
-  constexpr int ST_FULL = 32 * SPB;  // vector stores of a full tile's epilogue per wave
-  constexpr int ST_WAIT = ST_FULL < 63 ? ST_FULL : 63;
-  bool post = false;     // an epilogue ran since the last K-tile wait ...
-  bool st_full = true;   // ... and issued ST_FULL stores (else fewer: partial tile)
-
-  auto mfma_row = [&](int kk, int i) {
-#pragma unroll
-    for (int jb = 0; jb < 8; ++jb)
-      asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+a"(acc[i][jb]) : "v"(fb[kk][jb]), "v"(fa[kk][i]));
-  };
-
-  // prologue: K-tiles 0, 1 in flight, K-tile 0 landed; R0 <- K-tile 0 half 0
-#pragma unroll
-  for (int q = 0; q < 16; ++q) issue_piece(0, q);
-  advance_loader();
-  if (total > 1) {
-#pragma unroll
-    for (int q = 0; q < 16; ++q) issue_piece(1, q);
-    advance_loader();
-    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-  } else {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();  // also publishes sbias
-#pragma unroll
-  for (int b = 0; b < 8; ++b) {
-    fa[0][b] = *(const half8*)(smem + offA[0] + b * 2048);
-    fb[0][b] = *(const half8*)(smem + offB[0] + b * 2048);
-  }
-
-  int t = 0;
-  for (int tl = 0; tl < my_n; ++tl) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int jb = 0; jb < 8; ++jb) acc[i][jb] = f32x4{};
-    for (int kt = 0; kt < ktiles; ++kt, ++t) {
-      const char* cur = (const char*)smem + (t & 1) * G4_SLOT;
-      const char* nxt = (const char*)smem + ((t + 1) & 1) * G4_SLOT;
-      // half 0 on R0; R1 <- this K-tile's half 1
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        mfma_row(0, i);
-        fa[1][i] = *(const half8*)(cur + offA[1] + i * 2048);
-        fb[1][i] = *(const half8*)(cur + offB[1] + i * 2048);
-      }
-      __builtin_amdgcn_s_setprio(0);
-      // K-tile t + 1 landed (the only LDS-DMA in flight, plus the last epilogue's stores when
-      // one ran since: they are younger; waiting for at most 63 outstanding is still enough);
-      // every wave is done reading K-tile t
-      if (__builtin_expect(!post, 1)) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      } else if (st_full) {
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(ST_WAIT) : "memory");
-      } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      post = false;
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-      // half 1 on R1; R0 <- K-tile t + 1's half 0 (stale data past the stream's end, unused);
-      // K-tile t + 2's LDS-DMA into this K-tile's buffer, two pieces per row block
-      const bool more = t + 2 < total;
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        mfma_row(1, i);
-        fa[0][i] = *(const half8*)(nxt + offA[0] + i * 2048);
-        fb[0][i] = *(const half8*)(nxt + offB[0] + i * 2048);
-        if (more) {
-          issue_piece(t + 2, 2 * i);
-          issue_piece(t + 2, 2 * i + 1);
-        }
-      }
-      __builtin_amdgcn_s_setprio(0);
-      if (more) advance_loader();
-    }
-    // the epilogue reads acc through VALU / accvgpr moves the hazard recognizer cannot relate to
-    // the asm MFMAs: let the last ones retire first
-    asm volatile("s_nop 15\n\ts_nop 3" ::: "memory");
-    // epilogue: row m0 + 128 wr + 16 i + fr, columns n0 + 128 wc + 32 p + 8 fq + 0..7 from the
-    // block pair (2p, 2p + 1)
-    const int T = lo + sidx + tl * nbx;
-    const int tm = T / tiles_n;
-    const int m0 = tm * 256, n0 = (T - tm * tiles_n) * 256;
-    post = true;
-    st_full = m0 + 256 <= g.M;
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      const int n = n0 + 128 * wc + 32 * p + 8 * fq;
-      float bn[8];
-#pragma unroll
-      for (int r = 0; r < 8; ++r) bn[r] = sbias[n + r];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int m = m0 + 128 * wr + 16 * i + fr;
-        if (m < g.M) gemm_store8<EPI>(g, m, n, acc[i][2 * p], acc[i][2 * p + 1], bn);
-      }
-    }
-  }
+  if (wr == 0) bar();  // same barrier count for both groups
 }
 
 // ---------------------------------------------------------------------------
@@ -1031,33 +666,21 @@ __device__ __forceinline__ void ln_row4(f32x4 (&v)[4], int lane, int D, float ep
   ln_row4p(v, lane, D, eps, g4, b4, y32, y16);
 }
 
-// RPW rows per wave (consecutive): every row's loads and the gamma / beta chunks are issued
-// before the first reduction, so a wave keeps RPW rows of loads in flight and a ViT / config-5
-// LayerNorm fits the chip in one round of workgroups (RPW = 2: 12,800 rows -> 1,600
-// workgroups) instead of 1.6 rounds with a tail. Per-row arithmetic is unchanged.
-template <int RPW>
+// One wave per row: the row's loads and the gamma / beta chunks are issued before the first
+// reduction (two rows per wave measured slower: 14.3 vs 12.3 us per ViT LayerNorm).
 __global__ __launch_bounds__(256) void layernorm4_kernel(LayerNormArgs a) {
   const int lane = threadIdx.x & 63;
-  const int r0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW;
-  if (r0 >= a.rows) return;
-  f32x4 v[RPW][4];
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= a.rows) return;
+  const int src = a.gather ? a.gather[r] : r;
+  const f32x4* x = (const f32x4*)(a.x + (size_t)src * a.ldx);
+  f32x4 v[4];
 #pragma unroll
-  for (int rr = 0; rr < RPW; ++rr) {
-    const int r = r0 + rr < a.rows ? r0 + rr : r0;
-    const int src = a.gather ? a.gather[r] : r;
-    const f32x4* x = (const f32x4*)(a.x + (size_t)src * a.ldx);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) v[rr][j] = lane + 64 * j < (a.D >> 2) ? x[lane + 64 * j] : f32x4{};
-  }
+  for (int j = 0; j < 4; ++j) v[j] = lane + 64 * j < (a.D >> 2) ? x[lane + 64 * j] : f32x4{};
   f32x4 g4[4], b4[4];
   ln_params4(lane, a.D, a.gamma, a.beta, g4, b4);
-#pragma unroll
-  for (int rr = 0; rr < RPW; ++rr) {
-    const int r = r0 + rr;
-    if (r < a.rows)
-      ln_row4p(v[rr], lane, a.D, a.eps, g4, b4, a.y32 ? a.y32 + (size_t)r * a.D : nullptr,
-               a.y16 ? a.y16 + (size_t)r * a.D : nullptr);
-  }
+  ln_row4p(v, lane, a.D, a.eps, g4, b4, a.y32 ? a.y32 + (size_t)r * a.D : nullptr,
+           a.y16 ? a.y16 + (size_t)r * a.D : nullptr);
 }
 
 // ViT token assembly + pre_layrnorm in one pass (modeling_clip.py:212-217, :642):
@@ -1088,329 +711,13 @@ __global__ __launch_bounds__(256) void vit_embed_ln_kernel(const float* __restri
 }
 
 // ---------------------------------------------------------------------------
-// K4: multi-head attention for sequences up to 512 (K and V of the head f32 in LDS:
-// 2 L dh 4 bytes <= 160 KiB): one workgroup per (sequence, head), each thread takes query
-// rows i, i + blockDim, ... with an online softmax over the keys (key padding mask,
-// optional causal mask).
-// qkv: [B*L][3*D] f16 (q | k | v, head h at columns h*DH), out: [B*L][D] f16.
-template <int DH>
-__global__ __launch_bounds__(256) void attention_kernel(AttentionArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float sh[];
-  float* Ks = sh;                       // [L][DH]
-  float* Vs = sh + a.L * DH;            // [L][DH]
-  int* valid = (int*)(sh + 2 * a.L * DH);  // [L]
-  const int b = blockIdx.x / a.H, hd = blockIdx.x - (blockIdx.x / a.H) * a.H;
-  const int D = a.H * DH;
-  const size_t rs = (size_t)3 * D;
-  const _Float16* base = a.qkv + (size_t)b * a.L * rs;
-  for (int idx = threadIdx.x; idx < a.L * DH; idx += blockDim.x) {
-    const int t = idx / DH, d = idx - (idx / DH) * DH;
-    Ks[idx] = (float)base[t * rs + D + hd * DH + d];
-    Vs[idx] = (float)base[t * rs + 2 * D + hd * DH + d];
-  }
-  for (int t = threadIdx.x; t < a.L; t += blockDim.x) valid[t] = a.mask ? (a.mask[b * a.L + t] != 0) : 1;
-  __syncthreads();
-  for (int i = threadIdx.x; i < a.L; i += blockDim.x) {
-  float q[DH], o[DH];
-  const _Float16* qr = base + i * rs + hd * DH;
-#pragma unroll
-  for (int d = 0; d < DH; ++d) {
-    q[d] = (float)qr[d] * a.scale;
-    o[d] = 0.f;
-  }
-  float m = -INFINITY, l = 0.f;
-  const int jend = a.causal ? i + 1 : a.L;
-  for (int j = 0; j < jend; ++j) {
-    if (!valid[j]) continue;
-    const float* kr = Ks + j * DH;
-    float s = 0.f;
-#pragma unroll
-    for (int d = 0; d < DH; ++d) s = fmaf(q[d], kr[d], s);
-    const float mn = fmaxf(m, s);
-    const float alpha = __expf(m - mn);
-    const float p = __expf(s - mn);
-    l = l * alpha + p;
-    const float* vr = Vs + j * DH;
-#pragma unroll
-    for (int d = 0; d < DH; ++d) o[d] = fmaf(p, vr[d], o[d] * alpha);
-    m = mn;
-  }
-  const float inv = l > 0.f ? 1.f / l : 0.f;
-  _Float16* orow = a.out + ((size_t)b * a.L + i) * D + hd * DH;
-#pragma unroll
-  for (int d = 0; d < DH; ++d) orow[d] = (_Float16)(o[d] * inv);
-  }
-}
-
-// K4 (MFMA form) for L <= 64, head_dim 64 — the ViT-B/32 case (L = 50) and short text.
-// One wave per (sequence, head), 4 heads per workgroup. Sequence padded to 64.
-//   S^T = K . Q^T   (4 x 2x2 MFMA 32x32x16): lane owns query q = (l&31) + 32*qb, registers
-//                   hold keys (reg&3) + 8(reg>>2) + 4(l>>5) + 32*kb, so the row softmax over
-//                   keys is in-register plus one xor-32 shuffle (guide T12 "swapped QK^T").
-//   O   = P . V     (4 x 2x2 MFMA): the P accumulator registers 8t..8t+7 of key block kb are
-//                   the A fragment of k-step s = 2kb + t with the k order permuted
-//                   (element j <-> key 16s + 8(j>>2) + 4(l>>5) + (j&3); guide §3
-//                   "An accumulator tile as the next MFMA's operand"); V is gathered from
-//                   LDS in that same order. P is normalised by its row sum before the cast.
-__global__ __launch_bounds__(256) void attention_mfma64_kernel(AttentionArgs a) {
-  constexpr int DH = 64;
-  __shared__ __attribute__((aligned(16))) _Float16 Vs[4][64][DH];  // per-wave V tile (8 KiB)
-  const int lane = threadIdx.x & 63;
-  const int w = threadIdx.x >> 6;
-  const int hh = lane >> 5, r = lane & 31;
-  const int pair = blockIdx.x * 4 + w;
-  const bool active = pair < a.B * a.H;
-  const int b = active ? pair / a.H : 0, hd = active ? pair - (pair / a.H) * a.H : 0;
-  const int D = a.H * DH, L = a.L;
-  const size_t rs = (size_t)3 * D;
-  const _Float16* base = a.qkv + (size_t)b * L * rs;
-
-  // V tile -> LDS (row per lane, zero rows >= L)
-  {
-    const int key = lane;
-    half8* dst = (half8*)&Vs[w][key][0];
-    if (active && key < L) {
-      const half8* src = (const half8*)(base + (size_t)key * rs + 2 * D + hd * DH);
-#pragma unroll
-      for (int c = 0; c < 8; ++c) dst[c] = src[c];
-    } else {
-#pragma unroll
-      for (int c = 0; c < 8; ++c) dst[c] = half8{};
-    }
-  }
-  // K (A operand) and Q (B operand) fragments: row r + 32*blk, dims 16s + 8hh .. +7
-  half8 kf[2][4], qf[2][4];
-#pragma unroll
-  for (int blk = 0; blk < 2; ++blk) {
-    const int row = r + 32 * blk;
-    const bool ok = active && row < L;
-    const _Float16* kr = base + (size_t)row * rs + D + hd * DH + 8 * hh;
-    const _Float16* qr = base + (size_t)row * rs + hd * DH + 8 * hh;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      kf[blk][s] = ok ? *(const half8*)(kr + 16 * s) : half8{};
-      qf[blk][s] = ok ? *(const half8*)(qr + 16 * s) : half8{};
-    }
-  }
-  __syncthreads();
-  if (!active) return;
-
-  f32x16 st[2][2];  // [key block][query block]
-#pragma unroll
-  for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-    for (int qb = 0; qb < 2; ++qb) {
-      f32x16 acc = {};
-#pragma unroll
-      for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf[kb][s], qf[qb][s], acc, 0, 0, 0);
-      st[kb][qb] = acc;
-    }
-
-  // softmax over keys for the lane's two queries
-  half8 pa[2][4];  // [query block][k-step]
-#pragma unroll
-  for (int qb = 0; qb < 2; ++qb) {
-    const int q = r + 32 * qb;
-    float m = -INFINITY;
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-      for (int reg = 0; reg < 16; ++reg) {
-        const int key = (reg & 3) + 8 * (reg >> 2) + 4 * hh + 32 * kb;
-        bool ok = key < L;
-        if (a.mask) ok = ok && a.mask[(size_t)b * L + min(key, L - 1)] != 0;
-        if (a.causal) ok = ok && key <= q;
-        const float v = ok ? st[kb][qb][reg] * a.scale : -INFINITY;
-        st[kb][qb][reg] = v;
-        m = fmaxf(m, v);
-      }
-    m = fmaxf(m, __shfl_xor(m, 32));
-    float l = 0.f;
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-      for (int reg = 0; reg < 16; ++reg) {
-        const float pv = m == -INFINITY ? 0.f : __expf(st[kb][qb][reg] - m);
-        st[kb][qb][reg] = pv;
-        l += pv;
-      }
-    l += __shfl_xor(l, 32);
-    const float inv = l > 0.f ? 1.f / l : 0.f;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const int kb = s >> 1, t = s & 1;
-      half8 f;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) f[j] = (_Float16)(st[kb][qb][8 * t + j] * inv);
-      pa[qb][s] = f;
-    }
-  }
-  // V fragments in the permuted key order: element j <-> key 16s + 8(j>>2) + 4hh + (j&3)
-  half8 vf[2][4];  // [dim block][k-step]
-#pragma unroll
-  for (int db = 0; db < 2; ++db)
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      half8 f;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) f[j] = Vs[w][16 * s + 8 * (j >> 2) + 4 * hh + (j & 3)][r + 32 * db];
-      vf[db][s] = f;
-    }
-  _Float16* orow = a.out + (size_t)b * L * D + hd * DH;
-#pragma unroll
-  for (int qb = 0; qb < 2; ++qb)
-#pragma unroll
-    for (int db = 0; db < 2; ++db) {
-      f32x16 acc = {};
-#pragma unroll
-      for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(pa[qb][s], vf[db][s], acc, 0, 0, 0);
-#pragma unroll
-      for (int reg = 0; reg < 16; ++reg) {
-        const int q = (reg & 3) + 8 * (reg >> 2) + 4 * hh + 32 * qb;
-        if (q < L) orow[(size_t)q * D + r + 32 * db] = (_Float16)acc[reg];
-      }
-    }
-}
-
-// K4 v2 (MFMA form, L <= 64, head_dim 64 or 32): as v1 up to the softmax, then
-//   O^T = V^T . P^T: P^T is the S^T accumulator itself (registers 8t..8t+7 of key block kb
-//                   are the B fragment of k-step 2kb + t, key order permuted: element j <->
-//                   key 16s + 8(j>>2) + 4h + (j&3)); the V^T A fragments come from the row-major
-//                   V image by ds_read_b64_tr_b16 in that same order (two per fragment, 16 in
-//                   all; v1: 64 ds_read_u16).
-//   The O^T block has the query on the lane and 4 consecutive dims per register group:
-//   16 8-byte stores per lane (v1: 64 scattered 2-byte stores).
-// No block barrier: each wave owns its V image, and a wave past the end returns whole (the
-// transposed read needs EXEC all ones).
+// K4 helpers: transposed 16-bit LDS reads (ds_read_b64_tr_b16) for the V^T operand.
 typedef _Float16 half4_t __attribute__((ext_vector_type(4)));
 typedef __fp16 fp16x4_lds __attribute__((__vector_size__(8)));
 
 __device__ __forceinline__ half4_t lds_read_tr16(const _Float16* p) {
   const fp16x4_lds v = __builtin_amdgcn_ds_read_tr16_b64_v4f16((AS3 fp16x4_lds*)(p));
   return __builtin_bit_cast(half4_t, v);
-}
-
-template <int DH>  // 64 (CLIP) or 32 (MiniLM)
-__global__ __launch_bounds__(256) void attention_mfma64t_kernel(AttentionArgs a) {
-  constexpr int KS = DH / 16;  // 16-dim k-steps of S^T = K . Q^T
-  constexpr int DB = DH / 32;  // 32-dim output blocks of O^T
-  constexpr int LPR = DH / 8;  // lanes per V row (16 B each)
-  constexpr int VROW = 96;     // 192-byte rows: the 4 rows of one transposed read hit disjoint banks
-  __shared__ __attribute__((aligned(16))) _Float16 Vs[4][64 * VROW];
-  const int lane = threadIdx.x & 63;
-  const int w = threadIdx.x >> 6;
-  const int hh = lane >> 5, r = lane & 31;
-  const int pair = blockIdx.x * 4 + w;
-  if (pair >= a.B * a.H) return;
-  const int b = pair / a.H, hd = pair - (pair / a.H) * a.H;
-  const int D = a.H * DH, L = a.L;
-  const size_t rs = (size_t)3 * D;
-  const _Float16* base = a.qkv + (size_t)b * L * rs;
-  _Float16* vs = Vs[w];
-
-  // V rows -> LDS: 8 lanes x 16 B per row, 8 rows per instruction, zero rows >= L
-#pragma unroll
-  for (int it = 0; it < LPR; ++it) {  // LPR lanes x 16 B per row, 64 / LPR rows per instruction
-    const int key = (64 / LPR) * it + lane / LPR, c = lane % LPR;
-    half8 v = {};
-    if (key < L) v = *(const half8*)(base + (size_t)key * rs + 2 * D + hd * DH + 8 * c);
-    *(half8*)(vs + key * VROW + 8 * c) = v;
-  }
-  // K (A operand) and Q (B operand) fragments: row r + 32*blk, dims 16s + 8hh .. +7
-  half8 kf[2][KS], qf[2][KS];
-#pragma unroll
-  for (int blk = 0; blk < 2; ++blk) {
-    const int row = r + 32 * blk;
-    const bool ok = row < L;
-    const _Float16* kr = base + (size_t)row * rs + D + hd * DH + 8 * hh;
-    const _Float16* qr = base + (size_t)row * rs + hd * DH + 8 * hh;
-#pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      kf[blk][s] = ok ? *(const half8*)(kr + 16 * s) : half8{};
-      qf[blk][s] = ok ? *(const half8*)(qr + 16 * s) : half8{};
-    }
-  }
-  f32x16 st[2][2];  // [key block][query block]
-#pragma unroll
-  for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-    for (int qb = 0; qb < 2; ++qb) {
-      f32x16 acc = {};
-#pragma unroll
-      for (int s = 0; s < KS; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf[kb][s], qf[qb][s], acc, 0, 0, 0);
-      st[kb][qb] = acc;
-    }
-  // softmax over keys for the lane's two queries (as v1); P^T fragments in permuted key order
-  half8 pb[2][4];  // [query block][k-step]
-#pragma unroll
-  for (int qb = 0; qb < 2; ++qb) {
-    const int q = r + 32 * qb;
-    float m = -INFINITY;
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-      for (int reg = 0; reg < 16; ++reg) {
-        const int key = (reg & 3) + 8 * (reg >> 2) + 4 * hh + 32 * kb;
-        bool ok = key < L;
-        if (a.mask) ok = ok && a.mask[(size_t)b * L + min(key, L - 1)] != 0;
-        if (a.causal) ok = ok && key <= q;
-        const float v = ok ? st[kb][qb][reg] * a.scale : -INFINITY;
-        st[kb][qb][reg] = v;
-        m = fmaxf(m, v);
-      }
-    m = fmaxf(m, __shfl_xor(m, 32));
-    float l = 0.f;
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-      for (int reg = 0; reg < 16; ++reg) {
-        const float pv = m == -INFINITY ? 0.f : __expf(st[kb][qb][reg] - m);
-        st[kb][qb][reg] = pv;
-        l += pv;
-      }
-    l += __shfl_xor(l, 32);
-    const float inv = l > 0.f ? 1.f / l : 0.f;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const int kb = s >> 1, t = s & 1;
-      half8 f;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) f[j] = (_Float16)(st[kb][qb][8 * t + j] * inv);
-      pb[qb][s] = f;
-    }
-  }
-  // V^T fragments: 16-lane group g reads rows (keys) r0 .. r0 + 3, columns (dims) c0 + 4p .. + 3
-  // (lane 4q + p of the group supplies row q); lane i of the group receives dim c0 + i
-  const int g = lane >> 4, q4 = (lane & 15) >> 2, p4 = lane & 3;
-  half8 vf[DB][4];  // [dim block][k-step]
-#pragma unroll
-  for (int db = 0; db < DB; ++db)
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const _Float16* pa = vs + (16 * s + 4 * hh + q4) * VROW + 32 * db + 16 * (g & 1) + 4 * p4;
-      const half4_t lo = lds_read_tr16(pa), hi = lds_read_tr16(pa + 8 * VROW);
-      vf[db][s] = half8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-    }
-  _Float16* obase = a.out + (size_t)b * L * D + hd * DH;
-#pragma unroll
-  for (int qb = 0; qb < 2; ++qb) {
-    const int q = r + 32 * qb;
-#pragma unroll
-    for (int db = 0; db < DB; ++db) {
-      f32x16 acc = {};
-#pragma unroll
-      for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(vf[db][s], pb[qb][s], acc, 0, 0, 0);
-      // lane: query q, dims 32 db + 8 g4 + 4 hh + (0..3)
-      if (q < L) {
-#pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4) {
-          const half4_t h = {(_Float16)acc[4 * g4], (_Float16)acc[4 * g4 + 1], (_Float16)acc[4 * g4 + 2],
-                             (_Float16)acc[4 * g4 + 3]};
-          *(half4_t*)(obase + (size_t)q * D + 32 * db + 8 * g4 + 4 * hh) = h;
-        }
-      }
-    }
-  }
 }
 
 // K4 v3 (flash form, any L <= 512, head_dim 32 or 64): one wave per (sequence, head, 16-query
@@ -1426,7 +733,7 @@ __global__ __launch_bounds__(256) void attention_mfma64t_kernel(AttentionArgs a)
 // are skipped, and every other block is processed identically whatever the batch's length:
 // a sequence's result does not depend on how its batch is padded, for every L. Work per
 // (sequence, head) grows with its own length only, not with a 64-row pad.
-template <int DH, int PF = 0>  // PF 0: a key block's operands at its top; 1: two blocks ahead (A/B)
+template <int DH>
 __global__ __launch_bounds__(256) void attention_flash16_kernel(AttentionArgs a) {
   constexpr int KS = DH / 32;               // 32-dim k-steps of S^T
   constexpr int DB = DH / 16;               // 16-dim blocks of O^T
@@ -1454,9 +761,9 @@ __global__ __launch_bounds__(256) void attention_flash16_kernel(AttentionArgs a)
   float m = -INFINITY, l = 0.f;
   _Float16* vs = Vs[w];
   const int nkb = a.causal ? min((L + 15) >> 4, qb + 1) : (L + 15) >> 4;
-  // a key block's operands (K fragments, this lane's V chunks, its 4 keys' mask flags) are
-  // loaded two blocks ahead, so the per-block chain is compute only after the first block's
-  // load latency (it was K load -> MFMA -> V load -> LDS: two memory latencies per block)
+  // a key block's operands (K fragments, this lane's V chunks, its 4 keys' mask flags) are loaded
+  // together at its top (24.6 us per ViT layer vs 27.1 for a K -> MFMA -> V chain; two blocks
+  // ahead measured 27.0: the extra VGPRs halve the occupancy)
   struct Blk {
     half8 kf[KS], vv[KS];
     bool kv[4];
@@ -1481,17 +788,9 @@ __global__ __launch_bounds__(256) void attention_flash16_kernel(AttentionArgs a)
       x.kv[r] = ok;
     }
   };
-  Blk cur, n1, n2;
-  if (PF && nkb > 0) load_blk(0, n1);
-  if (PF && nkb > 1) load_blk(1, n2);
+  Blk cur;
   for (int kb = 0; kb < nkb; ++kb) {
-    if constexpr (PF) {
-      cur = n1;
-      n1 = n2;
-      if (kb + 2 < nkb) load_blk(kb + 2, n2);
-    } else {
-      load_blk(kb, cur);
-    }
+    load_blk(kb, cur);
     bool any_ok = false;
 #pragma unroll
     for (int r = 0; r < 4; ++r) any_ok |= cur.kv[r];
@@ -1616,19 +915,6 @@ __global__ __launch_bounds__(256) void vit_im2col32_kernel(const uint8_t* __rest
   }
 }
 
-// X[b*T + t] = (t == 0 ? cls : patch[b*(T-1) + t-1]) + pos[t]   (f32)
-__global__ void vit_assemble_kernel(const float* __restrict__ patch, const float* __restrict__ cls,
-                                    const float* __restrict__ pos, float* __restrict__ X, int B, int T, int D) {
-  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= (int64_t)B * T * D) return;
-  const int d = (int)(idx % D);
-  const int64_t bt = idx / D;
-  const int t = (int)(bt % T);
-  const int64_t b = bt / T;
-  const float e = t == 0 ? cls[d] : patch[(b * (T - 1) + t - 1) * D + d];
-  X[idx] = e + pos[(size_t)t * D + d];
-}
-
 // Token embeddings: X[b*T+t] = tok[ids] + pos[t] (+ type0 for BERT)   (f32)
 // one workgroup per token row (float4 over D): X[bt] = tok[id] + pos[t] (+ type row)
 __global__ __launch_bounds__(128) void token_embed_kernel(const int32_t* __restrict__ ids, const float* __restrict__ tok,
@@ -1703,16 +989,6 @@ __global__ void mean_pool_kernel(const float* __restrict__ X, const int32_t* __r
 
 // ---------------------------------------------------------------------------
 // launchers
-// env MRAG_GEMM_BIG (A/B timing): default -1 = K3d for M >= 1024 and N % 256 == 0, K3 otherwise;
-// 0 = K3 only. MRAG_GEMM_ABL: K3d ablation builds (timing only, EPI_F16).
-int gemm_big_mode() {
-  static const int v = [] {
-    const char* e = getenv("MRAG_GEMM_BIG");
-    return e ? atoi(e) : -1;
-  }();
-  return v;
-}
-
 int num_cus() {
   static int n = [] {
     int dev = 0, v = 0;
@@ -1723,239 +999,54 @@ int num_cus() {
   return n;
 }
 
-// K3d geometry: CFG 0 (256 x 256) unless env MRAG_G8_CFG=1 asks for CFG 1 (128 x 384) where
-// N % 384 == 0. CFG 1 fills 200 instead of 150 CUs at N = 768 but measured no faster (fc2
-// 97-99 us, out-proj 44 us either way; qkv 78 vs 59 us: notes/gemm_experiments.md), so the
-// persistent 256 x 256 kernel stays the default; CFG 1 is kept for A/B timing and is covered by
-// the parity tests (env-forced).
-int g8_pick_cfg(const GemmArgs& g) {
-  static const int force = [] {
-    const char* e = getenv("MRAG_G8_CFG");
-    return e ? atoi(e) : -1;
-  }();
-  if (force == 1 && g.N % 384 == 0) return 1;
-  return g.N % 256 == 0 ? 0 : -1;
-}
-
 // K3 (128 x 128, two workgroups per CU) vs K3d (persistent 256 x 256, one per CU) by rounds:
 // a K3 round (two tiles per CU) takes ~2/3 of a K3d round (one 4x larger tile) on the same K
 // (measured at K = 512 / 2048, N = 512: 23.7 vs 35.4 us, 53.1 vs 75.5 us), so K3 wins where the
 // 256 x 256 grid leaves CUs idle and the 128 x 128 one does not — the CLIP text tower at the
-// config-5 batch (N = 512). Both kernels accumulate every element in the same order.
+// config-5 batch (N = 512). Ties stay on K3d (ties to K3 measured slower on the overlapped
+// config-5 leg). Both kernels accumulate every element in the same order.
 bool k3_beats_k3d(const GemmArgs& g) {
   if (g.N % 256 != 0) return true;
   const long cus = std::max(8, num_cus() / 8 * 8);
   const long t256 = (long)((g.M + 255) / 256) * (g.N / 256), t128 = (long)((g.M + 127) / 128) * (g.N / 128);
   const long r_d = (t256 + cus - 1) / cus, r_3 = (t128 + 2 * cus - 1) / (2 * cus);
-  static const bool tie_k3 = [] {  // env MRAG_GEMM_TIE_K3=1: ties go to K3 (A/B timing)
-    const char* e = getenv("MRAG_GEMM_TIE_K3");
-    return e && atoi(e) == 1;
-  }();
-  return tie_k3 ? 2 * r_3 <= 3 * r_d : 2 * r_3 < 3 * r_d;  // K3 time ~ (2/3) r_3 < r_d; ties stay on K3d
+  return 2 * r_3 < 3 * r_d;  // K3 time ~ (2/3) r_3 < r_d
 }
 
-// K3d stream-K (SK) policy: env MRAG_G8_SK = 0 (default) off, 1 where the estimate says it
-// beats the data-parallel tile rounds, 2 wherever K3d runs (tests, A/B). Estimated in K-tile
-// steps per CU: DP = ceil(tiles / CUs) * k-tiles; SK = tiles * k-tiles / CUs, +15 % and +2
-// steps for the cut tiles' partial hand-off. Batches under 8192 rows keep the data-parallel
-// order (a row computed alone and inside such a batch is bit-identical). Measured SLOWER on
-// every ViT shape (fc2 106 -> 127 us, out-proj 46 -> 78, fc1 88 -> 109; CLIP 60.7k -> 46.8k
-// img/s, one box): a cut 256 x 256 tile hands off 256 KiB of f32 partials each way, ~110 MB
-// per out-proj launch against its 118 MB of operand fills (notes/gemm_experiments.md).
-int g8_sk_mode() {
-  static const int v = [] {
-    const char* e = getenv("MRAG_G8_SK");
-    return e ? atoi(e) : 0;
-  }();
-  return v;
-}
-
-bool g8_use_sk(const GemmArgs& g, int ntiles, int cus) {
-  const int mode = g8_sk_mode();
-  if (mode <= 0) return false;
-  if (mode >= 2) return true;
-  if (g.M < 8192) return false;
-  const double kt = g.K / GK;
-  const double dp = (double)((ntiles + cus - 1) / cus) * kt;
-  const double sk = 1.15 * ntiles * kt / cus + 2.0;
-  return sk < dp;
-}
-
-// Per-(device, stream) SK workspace: 2 partial slots per workgroup (grid <= CUs) and one
-// arrival counter per tile, zeroed once (every launch leaves them zero). Launches on one
-// stream are ordered, so they can share it; concurrent streams get their own.
-struct SkWorkspace {
-  float* part = nullptr;
-  int* cnt = nullptr;
-  int slots = 0, counters = 0;
-};
-
-int sk_workspace(hipStream_t s, int grid, int ntiles, GemmArgs& g) {
-  static std::mutex mu;
-  static std::map<std::pair<int, hipStream_t>, SkWorkspace> pool;
-  int dev = 0;
-  MRAG_HIP(hipGetDevice(&dev));
-  std::lock_guard<std::mutex> lk(mu);
-  SkWorkspace& w = pool[{dev, s}];
-  if (w.slots < 2 * grid) {
-    if (w.part) {
-      MRAG_HIP(hipStreamSynchronize(s));
-      MRAG_HIP(hipFree(w.part));
-      w.part = nullptr;
-      w.slots = 0;
-    }
-    MRAG_HIP(hipMalloc(&w.part, (size_t)2 * grid * SK_SLOT_BYTES));
-    w.slots = 2 * grid;
+template <template <int> class KERN>
+int launch_epi(int epi, dim3 grid, dim3 block, hipStream_t s, const GemmArgs& g) {
+  switch (epi) {
+    case EPI_F16: hipLaunchKernelGGL(KERN<EPI_F16>::fn, grid, block, 0, s, g); break;
+    case EPI_F16_QUICK_GELU: hipLaunchKernelGGL(KERN<EPI_F16_QUICK_GELU>::fn, grid, block, 0, s, g); break;
+    case EPI_F16_GELU_ERF: hipLaunchKernelGGL(KERN<EPI_F16_GELU_ERF>::fn, grid, block, 0, s, g); break;
+    case EPI_F32_RESIDUAL: hipLaunchKernelGGL(KERN<EPI_F32_RESIDUAL>::fn, grid, block, 0, s, g); break;
+    case EPI_F32: hipLaunchKernelGGL(KERN<EPI_F32>::fn, grid, block, 0, s, g); break;
+    default: return mrag::fail(MRAG_ERR_ARG, "gemm: bad epilogue %d", epi);
   }
-  if (w.counters < ntiles) {
-    if (w.cnt) {
-      MRAG_HIP(hipStreamSynchronize(s));
-      MRAG_HIP(hipFree(w.cnt));
-      w.cnt = nullptr;
-      w.counters = 0;
-    }
-    const int n = std::max(ntiles, 4096);
-    MRAG_HIP(hipMalloc(&w.cnt, (size_t)n * 4));
-    MRAG_HIP(hipMemsetAsync(w.cnt, 0, (size_t)n * 4, s));
-    w.counters = n;
-  }
-  g.sk_part = w.part;
-  g.sk_cnt = w.cnt;
+  MRAG_CHECK_LAUNCH();
   return MRAG_OK;
 }
-
 template <int EPI>
-int launch_gemm_8p_sk(const GemmArgs& g0, hipStream_t s) {
-  const int ntiles = ((g0.M + 255) / 256) * (g0.N / 256);
-  const int nb = std::max(8, num_cus() / 8 * 8);
-  GemmArgs g = g0;
-  if (int rc = sk_workspace(s, nb, ntiles, g)) return rc;
-  static bool said = false;
-  if (!said && getenv("MRAG_G8_VERBOSE")) {
-    fprintf(stderr, "K3d stream-K: %d CUs, grid %d for %d tiles x %d k-tiles\n", num_cus(), nb, ntiles, g.K / GK);
-    said = true;
-  }
-  hipLaunchKernelGGL((gemm_8p_kernel<EPI, 0, 0, 1>), dim3((unsigned)nb), dim3(G8_THREADS), 0, s, g);
-  MRAG_CHECK_LAUNCH();
-  return MRAG_OK;
-}
-
-template <int CFG>
-int launch_gemm_8p_cfg(const GemmArgs& g, int epi, hipStream_t s) {
-  using GG = G8Geom<CFG>;
-  const int ntiles = ((g.M + GG::BM - 1) / GG::BM) * (g.N / GG::BN);
-  if (CFG == 0 && g8_use_sk(g, ntiles, std::max(8, num_cus() / 8 * 8))) {
-    switch (epi) {
-      case EPI_F16: return launch_gemm_8p_sk<EPI_F16>(g, s);
-      case EPI_F16_QUICK_GELU: return launch_gemm_8p_sk<EPI_F16_QUICK_GELU>(g, s);
-      case EPI_F16_GELU_ERF: return launch_gemm_8p_sk<EPI_F16_GELU_ERF>(g, s);
-      case EPI_F32_RESIDUAL: return launch_gemm_8p_sk<EPI_F32_RESIDUAL>(g, s);
-      case EPI_F32: return launch_gemm_8p_sk<EPI_F32>(g, s);
-      default: return mrag::fail(MRAG_ERR_ARG, "gemm: bad epilogue %d", epi);
-    }
-  }
-  int nb = std::min((ntiles + 7) / 8 * 8, std::max(8, num_cus() / 8 * 8));
-  static const int grid_override = [] {
-    const char* e = getenv("MRAG_G8_GRID");
-    return e ? atoi(e) : 0;
-  }();
-  if (grid_override > 0) nb = std::min(nb, grid_override);
-  static bool said = false;
-  if (!said && getenv("MRAG_G8_VERBOSE")) {
-    fprintf(stderr, "K3d cfg %d: %d CUs, grid %d for %d tiles\n", CFG, num_cus(), nb, ntiles);
-    said = true;
-  }
-  const dim3 grid((unsigned)nb);
-  static const int abl = [] {
-    const char* e = getenv("MRAG_GEMM_ABL");
-    return e ? atoi(e) : 0;
-  }();
-  if (CFG == 0 && abl != 0 && epi == EPI_F16) {
-    switch (abl) {
-      case 1: hipLaunchKernelGGL((gemm_8p_kernel<EPI_F16, 1>), grid, dim3(G8_THREADS), 0, s, g); break;
-      case 2: hipLaunchKernelGGL((gemm_8p_kernel<EPI_F16, 2>), grid, dim3(G8_THREADS), 0, s, g); break;
-      case 3: hipLaunchKernelGGL((gemm_8p_kernel<EPI_F16, 3>), grid, dim3(G8_THREADS), 0, s, g); break;
-      case 5: hipLaunchKernelGGL((gemm_8p_kernel<EPI_F16, 5>), grid, dim3(G8_THREADS), 0, s, g); break;
-      case 7: hipLaunchKernelGGL((gemm_8p_kernel<EPI_F16, 7>), grid, dim3(G8_THREADS), 0, s, g); break;
-      case 8: hipLaunchKernelGGL((gemm_8p_kernel<EPI_F16, 8>), grid, dim3(G8_THREADS), 0, s, g); break;
-      default: hipLaunchKernelGGL((gemm_8p_kernel<EPI_F16, 4>), grid, dim3(G8_THREADS), 0, s, g); break;
-    }
-    MRAG_CHECK_LAUNCH();
-    return MRAG_OK;
-  }
-  switch (epi) {
-    case EPI_F16: hipLaunchKernelGGL((gemm_8p_kernel<EPI_F16, 0, CFG>), grid, dim3(G8_THREADS), 0, s, g); break;
-    case EPI_F16_QUICK_GELU:
-      hipLaunchKernelGGL((gemm_8p_kernel<EPI_F16_QUICK_GELU, 0, CFG>), grid, dim3(G8_THREADS), 0, s, g);
-      break;
-    case EPI_F16_GELU_ERF:
-      hipLaunchKernelGGL((gemm_8p_kernel<EPI_F16_GELU_ERF, 0, CFG>), grid, dim3(G8_THREADS), 0, s, g);
-      break;
-    case EPI_F32_RESIDUAL:
-      hipLaunchKernelGGL((gemm_8p_kernel<EPI_F32_RESIDUAL, 0, CFG>), grid, dim3(G8_THREADS), 0, s, g);
-      break;
-    case EPI_F32: hipLaunchKernelGGL((gemm_8p_kernel<EPI_F32, 0, CFG>), grid, dim3(G8_THREADS), 0, s, g); break;
-    default: return mrag::fail(MRAG_ERR_ARG, "gemm: bad epilogue %d", epi);
-  }
-  MRAG_CHECK_LAUNCH();
-  return MRAG_OK;
-}
-
-// K3e (4 waves of 128 x 128) instead of K3d where both apply: env MRAG_GEMM_4W=1 (A/B timing)
-int gemm_4w_mode() {
-  static const int v = [] {
-    const char* e = getenv("MRAG_GEMM_4W");
-    return e ? atoi(e) : 0;
-  }();
-  return v;
-}
-
-int launch_gemm_4w(const GemmArgs& g, int epi, hipStream_t s) {
-  const int ntiles = ((g.M + 255) / 256) * (g.N / 256);
-  const dim3 grid((unsigned)std::min((ntiles + 7) / 8 * 8, std::max(8, num_cus() / 8 * 8)));
-  switch (epi) {
-    case EPI_F16: hipLaunchKernelGGL(gemm_4w_kernel<EPI_F16>, grid, dim3(G4_THREADS), 0, s, g); break;
-    case EPI_F16_QUICK_GELU: hipLaunchKernelGGL(gemm_4w_kernel<EPI_F16_QUICK_GELU>, grid, dim3(G4_THREADS), 0, s, g); break;
-    case EPI_F16_GELU_ERF: hipLaunchKernelGGL(gemm_4w_kernel<EPI_F16_GELU_ERF>, grid, dim3(G4_THREADS), 0, s, g); break;
-    case EPI_F32_RESIDUAL: hipLaunchKernelGGL(gemm_4w_kernel<EPI_F32_RESIDUAL>, grid, dim3(G4_THREADS), 0, s, g); break;
-    case EPI_F32: hipLaunchKernelGGL(gemm_4w_kernel<EPI_F32>, grid, dim3(G4_THREADS), 0, s, g); break;
-    default: return mrag::fail(MRAG_ERR_ARG, "gemm: bad epilogue %d", epi);
-  }
-  MRAG_CHECK_LAUNCH();
-  return MRAG_OK;
-}
+struct K3dKern {
+  static constexpr auto fn = gemm_8p_kernel<EPI>;
+};
+template <int EPI>
+struct K3Kern {
+  static constexpr auto fn = gemm_nt_kernel<EPI>;
+};
 
 int launch_gemm(const GemmArgs& g, int epi, hipStream_t s) {
   if (g.M <= 0) return MRAG_OK;
   MRAG_REQUIRE(g.N % GN == 0 && g.K % GK == 0, "gemm: N=%d must be a multiple of %d and K=%d of %d", g.N, GN, g.K,
                GK);
   MRAG_REQUIRE(g.lda % 8 == 0 && g.ldw % 8 == 0 && g.ldc % 4 == 0, "gemm: lda/ldw must be multiples of 8, ldc of 4");
-  if (gemm_big_mode() != 0 && g.M >= 1024 && g.N <= G8_BIAS_MAX && !k3_beats_k3d(g)) {
-    // K3e needs 32-bit byte offsets into A and W (SADDR LDS-DMA)
-    if (gemm_4w_mode() == 1 && g.N % 256 == 0 && (long)g.M * g.lda * 2 < (1l << 31) &&
-        (long)g.N * g.ldw * 2 < (1l << 31))
-      return launch_gemm_4w(g, epi, s);
-    const int cfg = g8_pick_cfg(g);
-    if (cfg == 0) return launch_gemm_8p_cfg<0>(g, epi, s);
-    if (cfg == 1) return launch_gemm_8p_cfg<1>(g, epi, s);
+  if (g.M >= 1024 && g.N <= G8_BIAS_MAX && g.N % 256 == 0 && !k3_beats_k3d(g)) {
+    const int ntiles = ((g.M + G8Geom::BM - 1) / G8Geom::BM) * (g.N / G8Geom::BN);
+    const int nb = std::min((ntiles + 7) / 8 * 8, std::max(8, num_cus() / 8 * 8));
+    return launch_epi<K3dKern>(epi, dim3((unsigned)nb), dim3(G8_THREADS), s, g);
   }
   const dim3 grid((unsigned)(((g.M + GM - 1) / GM) * (g.N / GN)));
-  static const int k3_remap = [] {
-    const char* e = getenv("MRAG_K3_REMAP");
-    return e ? atoi(e) : 1;
-  }();
-  GemmArgs g3 = g;
-  g3.k3_remap = k3_remap;
-  switch (epi) {
-    case EPI_F16: hipLaunchKernelGGL(gemm_nt_kernel<EPI_F16>, grid, dim3(GTHREADS), 0, s, g3); break;
-    case EPI_F16_QUICK_GELU: hipLaunchKernelGGL(gemm_nt_kernel<EPI_F16_QUICK_GELU>, grid, dim3(GTHREADS), 0, s, g3); break;
-    case EPI_F16_GELU_ERF: hipLaunchKernelGGL(gemm_nt_kernel<EPI_F16_GELU_ERF>, grid, dim3(GTHREADS), 0, s, g3); break;
-    case EPI_F32_RESIDUAL: hipLaunchKernelGGL(gemm_nt_kernel<EPI_F32_RESIDUAL>, grid, dim3(GTHREADS), 0, s, g3); break;
-    case EPI_F32: hipLaunchKernelGGL(gemm_nt_kernel<EPI_F32>, grid, dim3(GTHREADS), 0, s, g3); break;
-    default: return mrag::fail(MRAG_ERR_ARG, "gemm: bad epilogue %d", epi);
-  }
-  MRAG_CHECK_LAUNCH();
-  return MRAG_OK;
+  return launch_epi<K3Kern>(epi, grid, dim3(GTHREADS), s, g);
 }
 
 int launch_layernorm(const LayerNormArgs& a, hipStream_t s) {
@@ -1963,14 +1054,8 @@ int launch_layernorm(const LayerNormArgs& a, hipStream_t s) {
   MRAG_REQUIRE(a.D > 0 && a.D <= 1024, "layernorm: D=%d unsupported", a.D);
   const bool vec4 = a.D % 4 == 0 && a.ldx % 4 == 0 && ((uintptr_t)a.x & 15) == 0 && ((uintptr_t)a.gamma & 15) == 0 &&
                     ((uintptr_t)a.beta & 15) == 0 && ((uintptr_t)a.y32 & 15) == 0 && ((uintptr_t)a.y16 & 7) == 0;
-  static const int rpw = [] {  // env MRAG_LN_RPW = 2: two rows per wave (measured slower: 14.3 vs 12.3 us)
-    const char* e = getenv("MRAG_LN_RPW");
-    return e && atoi(e) == 2 ? 2 : 1;
-  }();
-  if (vec4 && rpw == 2)
-    hipLaunchKernelGGL(layernorm4_kernel<2>, dim3((unsigned)((a.rows + 7) / 8)), dim3(256), 0, s, a);
-  else if (vec4)
-    hipLaunchKernelGGL(layernorm4_kernel<1>, dim3((unsigned)((a.rows + 3) / 4)), dim3(256), 0, s, a);
+  if (vec4)
+    hipLaunchKernelGGL(layernorm4_kernel, dim3((unsigned)((a.rows + 3) / 4)), dim3(256), 0, s, a);
   else
     hipLaunchKernelGGL(layernorm_kernel, dim3((unsigned)((a.rows + 3) / 4)), dim3(256), 0, s, a);
   MRAG_CHECK_LAUNCH();
@@ -1987,77 +1072,14 @@ int launch_vit_embed_ln(const float* patch, const float* cls, const float* pos, 
   return MRAG_OK;
 }
 
-// MRAG_ATTN_VALU=1 forces the VALU form everywhere (cross-check in tests).
-bool force_valu_attention() {
-  static const bool v = [] {
-    const char* e = getenv("MRAG_ATTN_VALU");
-    return e && atoi(e) == 1;
-  }();
-  return v;
-}
-
-bool mfma_attention_dh32() {
-  static const bool v = [] {
-    const char* e = getenv("MRAG_ATTN_DH32");
-    return e && atoi(e) == 1;
-  }();
-  return v;
-}
-
 int launch_attention(const AttentionArgs& a, int dh, hipStream_t s) {
   if (a.B <= 0) return MRAG_OK;
   MRAG_REQUIRE(a.L >= 1 && a.L <= 512, "attention: L=%d unsupported (1..512)", a.L);
-  const size_t shm = (size_t)2 * a.L * dh * 4 + (size_t)a.L * 4;
-  MRAG_REQUIRE(shm <= 160 * 1024, "attention: L*dh too large for LDS");
-  const int threads = std::min(256, (a.L + 63) / 64 * 64);
-  const dim3 grid((unsigned)(a.B * a.H));
-  // K/V of a head stay f32 in LDS; above 64 KiB the kernel must opt in (gfx950: 160 KiB/CU)
-  static bool attr_set = false;
-  if (!attr_set) {
-    MRAG_HIP(hipFuncSetAttribute((const void*)attention_kernel<64>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                 160 * 1024));
-    MRAG_HIP(hipFuncSetAttribute((const void*)attention_kernel<32>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                 160 * 1024));
-    attr_set = true;
-  }
-  static const bool attn_v1 = [] {
-    const char* e = getenv("MRAG_ATTN_V1");
-    return e && atoi(e) == 1;
-  }();
-  static const bool legacy = [] {  // MRAG_ATTN_LEGACY=1: the round-1 dispatch (A/B timing)
-    const char* e = getenv("MRAG_ATTN_LEGACY");
-    return e && atoi(e) == 1;
-  }();
-  if ((dh == 64 || dh == 32) && !legacy && !force_valu_attention()) {
-    const int64_t items = (int64_t)a.B * a.H * ((a.L + 15) / 16);
-    MRAG_REQUIRE(items < (1ll << 33), "attention: batch too large");
-    const dim3 g4((unsigned)((items + 3) / 4));
-    // operands of a key block loaded together at its top (24.4 us per ViT layer vs 27.1 for the
-    // round-1 K -> MFMA -> V chain); MRAG_ATTN_PREFETCH=1 loads them two blocks ahead instead,
-    // which measured slower (27.0 us: 112 VGPRs halve the occupancy)
-    static const bool no_prefetch = [] {
-      const char* e = getenv("MRAG_ATTN_PREFETCH");
-      return !(e && atoi(e) == 1);
-    }();
-    auto kern = dh == 64 ? (no_prefetch ? attention_flash16_kernel<64, 0> : attention_flash16_kernel<64, 1>)
-                         : (no_prefetch ? attention_flash16_kernel<32, 0> : attention_flash16_kernel<32, 1>);
-    hipLaunchKernelGGL(kern, g4, dim3(256), 0, s, a);
-  } else if (dh == 64 && a.L <= 64 && !force_valu_attention() && !attn_v1) {
-    hipLaunchKernelGGL(attention_mfma64t_kernel<64>, dim3((unsigned)((a.B * a.H + 3) / 4)), dim3(256), 0, s, a);
-  } else if (dh == 32 && a.L <= 64 && mfma_attention_dh32()) {
-    // opt-in (MRAG_ATTN_DH32=1): the BERT towers otherwise stay on the f32 VALU kernel for every
-    // L, so a sequence's result does not depend on whether its batch pads past 64 tokens
-    // (cross-encoder predict(pair) == predict(batch)[i] to 1e-6)
-    hipLaunchKernelGGL(attention_mfma64t_kernel<32>, dim3((unsigned)((a.B * a.H + 3) / 4)), dim3(256), 0, s, a);
-  } else if (dh == 64 && a.L <= 64 && !force_valu_attention()) {
-    hipLaunchKernelGGL(attention_mfma64_kernel, dim3((unsigned)((a.B * a.H + 3) / 4)), dim3(256), 0, s, a);
-  } else if (dh == 64) {
-    hipLaunchKernelGGL(attention_kernel<64>, grid, dim3(threads), shm, s, a);
-  } else if (dh == 32) {
-    hipLaunchKernelGGL(attention_kernel<32>, grid, dim3(threads), shm, s, a);
-  } else {
-    return mrag::fail(MRAG_ERR_UNSUPPORTED, "attention: head_dim %d unsupported (32, 64)", dh);
-  }
+  MRAG_REQUIRE(dh == 64 || dh == 32, "attention: head_dim %d unsupported (32, 64)", dh);
+  const int64_t items = (int64_t)a.B * a.H * ((a.L + 15) / 16);
+  MRAG_REQUIRE(items < (1ll << 33), "attention: batch too large");
+  hipLaunchKernelGGL(dh == 64 ? attention_flash16_kernel<64> : attention_flash16_kernel<32>,
+                     dim3((unsigned)((items + 3) / 4)), dim3(256), 0, s, a);
   MRAG_CHECK_LAUNCH();
   return MRAG_OK;
 }
@@ -2072,16 +1094,6 @@ int launch_vit_im2col(const uint8_t* img, _Float16* out, int B, int S, int P, hi
     return MRAG_OK;
   }
   hipLaunchKernelGGL(vit_im2col_kernel, dim3((unsigned)((total8 + 255) / 256)), dim3(256), 0, s, img, out, B, S, P);
-  MRAG_CHECK_LAUNCH();
-  return MRAG_OK;
-}
-
-int launch_vit_assemble(const float* patch, const float* cls, const float* pos, float* X, int B, int T, int D,
-                        hipStream_t s) {
-  const int64_t n = (int64_t)B * T * D;
-  if (n == 0) return MRAG_OK;
-  hipLaunchKernelGGL(vit_assemble_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, patch, cls, pos, X, B,
-                     T, D);
   MRAG_CHECK_LAUNCH();
   return MRAG_OK;
 }

@@ -49,6 +49,7 @@ constexpr int QPG = SCAN_WAVES * QPW;       // queries per workgroup
 constexpr int MAX_MERGE_ENTRIES = 4096;     // splits * KL cap (LDS sort in K8)
 constexpr int MAX_K = 256;
 constexpr int MERGE_THREADS = 256;
+constexpr int SAMPLE_STRIDE = 16;          // K7 sample pre-pass: every 16th tile of a split
 
 // |approx - exact| bound for the fp16 scan:
 //   fp16 rounding of both unit vectors: (2u + u^2) * sum|q_i x_i| <= 9.77e-4 (u = 2^-11)
@@ -73,7 +74,7 @@ struct ScanParams {
   int ccap;
   // shared per-query rejection threshold (ordered-uint f32, 0 == none), top-k mode
   uint32_t* theta;
-  // sample pre-pass (v2 MODE 1): tiles split + i * splits * sample_stride, i < sample_tiles
+  // sample pre-pass (v3 MODE 1): tiles split + i * splits * sample_stride, i < sample_tiles
   int sample_tiles, sample_stride;
   // v3: requested k (publishing rule) and per-(split, query) bound on every dropped row
   int k;
@@ -160,7 +161,7 @@ __device__ __forceinline__ float masked_max16(const f32x16& a, uint64_t lane_mas
 // mask from one ballot over the tile's labels, the max of each lane's 32 scores,
 // and ONE wave-level test against the lane's rejection threshold; the per-row list
 // insertion runs only when some lane of the wave has a score above its threshold.
-template <int DP, int KL, bool COLLECT, bool ABLATE = false>
+template <int DP, int KL, bool COLLECT>
 __global__ __launch_bounds__(SCAN_THREADS) void knn_scan_kernel(ScanParams p) {
   constexpr int KSTEPS = DP / 16;
   constexpr int ROW_BYTES = DP * 2;
@@ -312,9 +313,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void knn_scan_kernel(ScanParams p) {
           acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, qf[kk], acc0, 0, 0, 0);
           acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, qf[kk], acc1, 0, 0, 0);
         }
-        if constexpr (ABLATE) {
-          asm volatile("" ::"v"(acc0[0]), "v"(acc0[7]), "v"(acc1[3]), "v"(acc1[15]));
-        } else {
+        {
           float m;
           if (tile_mask == ~0ull) {
             m = fmaxf(max16(acc0), max16(acc1));
@@ -371,33 +370,10 @@ __global__ __launch_bounds__(SCAN_THREADS) void knn_scan_kernel(ScanParams p) {
   }
 }
 
-// ---------------------------------------------------------------------------
-// K7 v2 (top-k mode, KL = 8): 4 waves x 64 queries per workgroup, one wave per SIMD.
-//
-// Why: in v1 every A fragment read from LDS feeds ONE MFMA (32 queries per wave, the
-// query fragments fill the 256-VGPR budget of 2 waves/SIMD), MFMAs wait on their
-// ds_reads, and the per-tile filter / list insertion (which fires in most tiles: a lane's
-// threshold is only its own list's KL-th or the best published one) runs between the
-// tile's MFMAs instead of beside them. Here:
-//  * the 64 queries' B fragments (DP/2 registers per lane: all 256 AGPRs at DP=512) live
-//    in the accumulator file for the whole launch — the MFMA takes B from AGPRs (inline
-//    asm with an "a" operand; hipcc loads them straight into a[...]) — so each A fragment
-//    feeds two MFMAs and the VGPR file is free for double-buffered accumulators;
-//  * A fragments are read two k-steps ahead into a 3-deep register ring;
-//  * the accumulators are double-buffered: while the MFMAs of tile t run, the filter of
-//    tile t-1 runs in the gaps between them (order pinned by sched_barrier). At one wave
-//    per SIMD only ~5 single-issue instructions hide behind one 32x32x16 MFMA, so each gap
-//    carries at most one job: the k-step's two A-fragment reads (gap 0), one next-tile
-//    LDS-DMA piece (gap 1), or one group test (gap 3): max of 8 of the lane's 64 scores
-//    against its threshold, one wave-uniform branch, and only on a hit the per-row list
-//    insertion of those 8 rows;
-//  * the shared threshold is seeded by the sample pre-pass (MODE 1) near the k-th best,
-//    so hits — and therefore insertions — are rare from the first tile on.
-// Semantics are identical to v1 (same lists, same shared threshold, same outputs).
 constexpr int SCAN2_WAVES = 4;
 constexpr int SCAN2_THREADS = SCAN2_WAVES * 64;
 constexpr int QPW2 = 64;  // two 32-query blocks per wave
-static_assert(SCAN2_WAVES * QPW2 == QPG, "v2 keeps the query-group size of v1");
+static_assert(SCAN2_WAVES * QPW2 == QPG, "v3 keeps the query-group size of v1");
 
 template <typename F, int... I>
 __device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
@@ -407,309 +383,6 @@ template <int N, typename F>
 __device__ __forceinline__ void static_for(F&& f) {
   static_for_impl(f, std::make_integer_sequence<int, N>{});
 }
-
-// acc += A.B with B resident in AGPRs (hipcc does not model asm: the caller guarantees
-// the MFMA->VALU distance with mfma_guard before any VALU reads `acc`).
-__device__ __forceinline__ void mfma_ab(f32x16& acc, const half8& a, const half8& b) {
-  asm volatile("v_mfma_f32_32x32x16_f16 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "a"(b));
-}
-__device__ __forceinline__ void mfma_ab0(f32x16& acc, const half8& a, const half8& b) {
-  asm volatile("v_mfma_f32_32x32x16_f16 %0, %1, %2, 0" : "=&v"(acc) : "v"(a), "a"(b));
-}
-// >= 18 wait states after the last MFMA writing these accumulators (8-pass XDL -> VALU).
-__device__ __forceinline__ void mfma_guard(f32x16 (&acc)[2][2]) {
-  asm volatile("s_nop 15\n\ts_nop 3" : "+v"(acc[0][0]), "+v"(acc[0][1]), "+v"(acc[1][0]), "+v"(acc[1][1]));
-}
-
-// ABL (timing experiments only, env MRAG_SCAN_ABLATE=10+ABL): 1 = no epilogue, 2 = fast filter
-// only, 3 = no epilogue + next-tile LDS-DMA issued 4 per k-step, 4 = no epilogue, no LDS-DMA.
-//
-// MODE 1 = the sample pre-pass: the same MFMA pipeline over a strided 1/sample_stride of each
-// split's tiles, keeping only each lane's running max (no lists, no inserts); the
-// per-(query, split, half) maxima go to part_s[(split * Qp + slot) * 2 + h] for
-// theta_init_kernel, which seeds the shared threshold with the k-th largest of them.
-template <int DP, int ABL = 0, int MODE = 0>
-__global__ __launch_bounds__(SCAN2_THREADS) void knn_scan2_kernel(ScanParams p) {
-  constexpr int KL = 8;
-  constexpr int KSTEPS = DP / 16;
-  constexpr int ROW_BYTES = DP * 2;
-  constexpr int TILE_BYTES = TILE_ROWS * ROW_BYTES;
-  constexpr int CPR = DP / 8;
-  constexpr int GLDS_PER_WAVE = TILE_BYTES / 1024 / SCAN2_WAVES;
-  static_assert(TILE_BYTES % (1024 * SCAN2_WAVES) == 0, "tile must split into 1 KiB pieces");
-  constexpr bool NO_EPI = ABL == 1 || ABL == 3 || ABL == 4;
-  constexpr bool NO_GLDS = ABL == 4;
-  static_assert(KSTEPS % GLDS_PER_WAVE == 0, "LDS-DMA pieces spread evenly over the k-steps");
-  static_assert(CPR % 16 == 0, "swizzle needs rows of a multiple of 16 chunks");
-  constexpr int NGROUPS = 8;  // group g: query block g>>2, row block (g>>1)&1, regs 8(g&1)..+8
-  static_assert(KSTEPS % NGROUPS == 0, "one group test every KSTEPS/8 k-steps");
-  constexpr int LBL_OFF = 2 * TILE_BYTES;
-  __shared__ __attribute__((aligned(16))) char smem[2 * TILE_BYTES + 2 * TILE_ROWS * 4];
-
-  const int lane = threadIdx.x & 63;
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int h = lane >> 5;
-  const int r32 = lane & 31;
-  const uint32_t lds_base = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)((AS3 char*)smem));
-
-  int qg, split;  // same XCD-aware block mapping as v1
-  {
-    const int b = blockIdx.x;
-    if ((p.splits & 7) == 0) {
-      const int xcd = b & 7, sl = b >> 3;
-      qg = sl % p.qgroups;
-      split = (sl / p.qgroups) * 8 + xcd;
-    } else {
-      qg = b % p.qgroups;
-      split = b / p.qgroups;
-    }
-  }
-  // query slot of block qb is slot0 + 32 qb; Qp is a multiple of QPG so every slot exists
-  const int slot0 = qg * QPG + w * QPW2 + r32;
-
-  half8 qf[KSTEPS][2];
-#pragma unroll
-  for (int kk = 0; kk < KSTEPS; ++kk)
-#pragma unroll
-    for (int qb = 0; qb < 2; ++qb)
-      qf[kk][qb] = *(const half8*)(p.q16 + (size_t)(slot0 + 32 * qb) * DP + kk * 16 + h * 8);
-  // retire the loads here (see v1): a visible use before the loop
-#pragma unroll
-  for (int kk = 0; kk < KSTEPS; ++kk) asm volatile("" ::"a"(qf[kk][0]), "a"(qf[kk][1]));
-
-  float ls[2][KL];
-  int li[2][KL];
-#pragma unroll
-  for (int qb = 0; qb < 2; ++qb)
-#pragma unroll
-    for (int j = 0; j < KL; ++j) {
-      ls[qb][j] = -INFINITY;
-      li[qb][j] = -1;
-    }
-  float theta_f[2] = {-INFINITY, -INFINITY};
-  uint32_t theta_next[2] = {0u, 0u};
-  float published[2] = {-INFINITY, -INFINITY};
-  uint32_t* const theta_q = p.theta + slot0;
-
-  // A-fragment chunk (2j + h) of row r32 sits at chunk (2j + h) ^ (r32 & 15): byte offset
-  // offA0 ^ (j << 5), with offA0 = r32 * ROW_BYTES + 16 * (h ^ (r32 & 15))
-  const int offA0_init = r32 * ROW_BYTES + 16 * (h ^ (r32 & 15));
-
-  // acc[buffer][row block][query block]; buffer 1 starts at -inf so the first tile's
-  // (empty) predecessor epilogue is a no-op without a branch.
-  f32x16 acc[2][2][2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[1][i][j][r] = -INFINITY;
-      acc[0][i][j] = f32x16{};
-    }
-
-  int my_tiles = (split < p.ntiles) ? (p.ntiles - 1 - split) / p.splits + 1 : 0;
-  int tstep = p.splits;
-  if constexpr (MODE == 1) {
-    my_tiles = min(my_tiles, p.sample_tiles);
-    tstep = p.splits * p.sample_stride;
-  }
-  float smax[2] = {-INFINITY, -INFINITY};  // MODE 1: running max per query block
-
-  // `lane_t` is `lane` made opaque once per tile, so the per-piece source offsets and the
-  // A-fragment offsets are recomputed where they are used instead of being hoisted out of
-  // the tile loop into ~40 loop-carried registers
-  auto stage_piece = [&](int buf, int tile, int i, int lane_t) {
-    const char* gt = (const char*)p.x16 + (size_t)tile * TILE_BYTES;
-    const unsigned piece = w * GLDS_PER_WAVE + i;
-    const unsigned P = piece * 64 + (unsigned)lane_t;
-    const unsigned row = P / CPR;
-    const unsigned pos = P - row * CPR;
-    const unsigned c = pos ^ (row & 15);
-    glds_x4(gt + row * ROW_BYTES + c * 16, lds_base + buf * TILE_BYTES + piece * 1024);
-  };
-  // DP = 512: piece i of wave w is corpus row w * 16 + i of the tile, so its source is one
-  // per-tile SGPR base + a lane offset 16 * (lane ^ i) + 1024 i (one VALU op per piece)
-  auto stage_row = [&](const char* gw, uint32_t ldsw, int i, uint32_t lane16) {
-    glds_x4_saddr((lane16 ^ (uint32_t)(i << 4)) + (uint32_t)(i * 1024), gw, ldsw + i * 1024);
-  };
-  auto stage_labels = [&](int buf, int tile) {
-    if (w == 0) glds_x1(p.labels + (size_t)tile * TILE_ROWS + lane, lds_base + LBL_OFF + buf * TILE_ROWS * 4);
-  };
-
-  // ---- epilogue of the previous tile: 8 group tests --------------------------------------
-  int prow = 0;  // first row of the filtered tile + 4h (its invalid rows are already -inf)
-
-  auto epi_group = [&](auto g_c, auto y_c) {
-    constexpr int G = decltype(g_c)::value;
-    constexpr int Y = decltype(y_c)::value;
-    constexpr int qb = G >> 2, rb = (G >> 1) & 1, r0 = 8 * (G & 1);
-    f32x16& av = acc[Y][rb][qb];
-    if constexpr (NO_EPI) {
-      asm volatile("" ::"v"(av));
-    } else {
-      float gm = fmaxf(fmaxf(fmaxf(av[r0], av[r0 + 1]), fmaxf(av[r0 + 2], av[r0 + 3])),
-                       fmaxf(fmaxf(av[r0 + 4], av[r0 + 5]), fmaxf(av[r0 + 6], av[r0 + 7])));
-      if constexpr (MODE == 1) {
-        smax[qb] = fmaxf(smax[qb], gm);
-        asm volatile("" : "+v"(smax[qb]));  // keep the slice in its gap
-      } else {
-        const bool hit = __any(gm > fmaxf(ls[qb][KL - 1], theta_f[qb]));
-        if (ABL != 2 && hit) {
-#pragma unroll
-          for (int r = r0; r < r0 + 8; ++r) {
-            const float sv = av[r];
-            if (sv > fmaxf(ls[qb][KL - 1], theta_f[qb]))
-              list_insert<KL>(ls[qb], li[qb], sv, prow + rb * 32 + 8 * (r >> 2) + (r & 3));
-          }
-          if (li[qb][KL - 1] >= 0 && ls[qb][KL - 1] > published[qb]) {
-            published[qb] = ls[qb][KL - 1];
-            __hip_atomic_fetch_max(theta_q + 32 * qb, mrag_f2ord(published[qb]), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-          }
-        }
-      }
-    }
-  };
-
-  // ---- one tile: MFMAs into acc[X] + the epilogue of acc[Y] in their shadow -----------
-  auto tile_body = [&](auto x_c, int it) {
-    constexpr int X = decltype(x_c)::value;
-    constexpr int Y = 1 - X;
-    const int tile = split + it * tstep;
-    const bool has_next = it + 1 < my_tiles;
-    // source of the next tile's pieces (the last tile restages itself into the idle buffer
-    // instead of branching around every piece)
-    const int ntile = has_next ? tile + tstep : tile;
-    const char* gw = (const char*)p.x16 + (size_t)ntile * TILE_BYTES + (size_t)w * GLDS_PER_WAVE * ROW_BYTES;
-    uint32_t ldsw = lds_base + Y * TILE_BYTES + w * GLDS_PER_WAVE * 1024;
-    asm volatile("" : "+s"(gw), "+s"(ldsw));
-    if constexpr (MODE == 0) {
-#pragma unroll
-      for (int qb = 0; qb < 2; ++qb)
-        theta_next[qb] = __hip_atomic_load(theta_q + 32 * qb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    const int lab = ((const int*)(smem + LBL_OFF + X * TILE_ROWS * 4))[lane];
-    const bool lab_ok = (p.label_filter == MRAG_LABEL_ANY) ? (lab >= 0) : (lab == p.label_filter);
-    const uint64_t tile_mask = __ballot(lab_ok);
-    const char* tb = smem + X * TILE_BYTES;
-    int lane_t = lane, offA0 = offA0_init;
-    uint32_t lane16 = lane * 16;
-    asm volatile("" : "+v"(lane_t), "+v"(offA0), "+v"(lane16));
-    half8 a[3][2];
-    auto read_a = [&](int slot, int kk) {
-      const int o = (offA0 ^ ((kk & 7) << 5)) + (kk >> 3) * 256;
-      a[slot][0] = *(const half8*)(tb + o);
-      a[slot][1] = *(const half8*)(tb + o + 32 * ROW_BYTES);
-    };
-    read_a(0, 0);
-    if (KSTEPS > 1) read_a(1, 1);
-    stage_labels(Y, ntile);
-    static_for<KSTEPS>([&](auto kk_c) {
-      constexpr int kk = decltype(kk_c)::value;
-      static_for<4>([&](auto j_c) {
-        constexpr int j = decltype(j_c)::value;
-        constexpr int rb = j >> 1, qb = j & 1;
-        if constexpr (kk == 0)
-          mfma_ab0(acc[X][rb][qb], a[kk % 3][rb], qf[kk][qb]);
-        else
-          mfma_ab(acc[X][rb][qb], a[kk % 3][rb], qf[kk][qb]);
-        // one job per MFMA gap (see the header)
-        constexpr int GLDS_EVERY = KSTEPS / GLDS_PER_WAVE;
-        constexpr int GROUP_EVERY = KSTEPS / NGROUPS;
-        if constexpr (j == 0) {
-          if constexpr (kk + 2 < KSTEPS) read_a((kk + 2) % 3, kk + 2);
-        } else if constexpr (j == 1) {
-          if constexpr (kk % GLDS_EVERY == 0 && !NO_GLDS) {
-            if constexpr (CPR == 64)
-              stage_row(gw, ldsw, kk / GLDS_EVERY, lane16);
-            else
-              stage_piece(Y, ntile, kk / GLDS_EVERY, lane_t);
-          }
-        } else if constexpr (j == 3) {
-          if constexpr (kk % GROUP_EVERY == 0)
-            epi_group(std::integral_constant<int, kk / GROUP_EVERY>{}, std::integral_constant<int, Y>{});
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      });
-    });
-    mfma_guard(acc[X]);
-    // rows failing the label filter drop out here (rare for unfiltered searches; kept
-    // out of the slots so its bit tests do not hold registers across the MFMA loop)
-    if (tile_mask != ~0ull) {
-      const uint64_t lm = tile_mask >> (4 * h);
-#pragma unroll
-      for (int rb = 0; rb < 2; ++rb)
-#pragma unroll
-        for (int reg = 0; reg < 16; ++reg) {
-          const bool ok = row_ok(lm, rb, reg);
-          acc[X][rb][0][reg] = ok ? acc[X][rb][0][reg] : -INFINITY;
-          acc[X][rb][1][reg] = ok ? acc[X][rb][1][reg] : -INFINITY;
-        }
-    }
-    // the filtered tile is now this one
-    prow = tile * TILE_ROWS + 4 * h;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    // fold in the threshold loaded at the top of this tile, here where the load has
-    // retired (used from the next tile on; pinned so hipcc's wait for it cannot land
-    // mid-tile, where it would also drain the LDS-DMA prefetch)
-    if constexpr (MODE == 0) {
-#pragma unroll
-      for (int qb = 0; qb < 2; ++qb)
-        if (theta_next[qb] != 0) theta_f[qb] = fmaxf(theta_f[qb], mrag_ord2f(theta_next[qb]));
-      asm volatile("" : "+v"(theta_f[0]), "+v"(theta_f[1]));
-    }
-    __syncthreads();
-  };
-
-  if (my_tiles > 0) {
-#pragma unroll
-    for (int i = 0; i < GLDS_PER_WAVE; ++i) stage_piece(0, split, i, lane);
-    stage_labels(0, split);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    for (int it = 0; it < my_tiles; it += 2) {
-      tile_body(std::integral_constant<int, 0>{}, it);
-      if (it + 1 < my_tiles) tile_body(std::integral_constant<int, 1>{}, it + 1);
-    }
-    // epilogue of the last tile
-    if (my_tiles & 1) {
-      static_for<NGROUPS>([&](auto g_c) { epi_group(g_c, std::integral_constant<int, 0>{}); });
-    } else {
-      static_for<NGROUPS>([&](auto g_c) { epi_group(g_c, std::integral_constant<int, 1>{}); });
-    }
-  }
-
-  if constexpr (MODE == 1) {
-#pragma unroll
-    for (int qb = 0; qb < 2; ++qb) p.part_s[((size_t)split * p.Qp + slot0 + 32 * qb) * 2 + h] = smax[qb];
-    return;
-  }
-  // fold the partner half-wave's lists (same queries, other rows) into lanes 0..31
-#pragma unroll
-  for (int qb = 0; qb < 2; ++qb) {
-    float ps[KL];
-    int pi[KL];
-#pragma unroll
-    for (int j = 0; j < KL; ++j) {
-      ps[j] = __shfl_xor(ls[qb][j], 32);
-      pi[j] = __shfl_xor(li[qb][j], 32);
-    }
-    if (h == 0) {
-#pragma unroll
-      for (int j = 0; j < KL; ++j)
-        if (ps[j] > ls[qb][KL - 1]) list_insert<KL>(ls[qb], li[qb], ps[j], pi[j]);
-      const int slot = slot0 + 32 * qb;
-      float* os = p.part_s + ((size_t)split * p.Qp + slot) * KL;
-      int32_t* oi = p.part_i + ((size_t)split * p.Qp + slot) * KL;
-#pragma unroll
-      for (int j = 0; j < KL; ++j) {
-        os[j] = ls[qb][j];
-        oi[j] = li[qb][j];
-      }
-    }
-  }
-}
-
 // ---------------------------------------------------------------------------
 // K7 v3 (top-k mode): v2's pipeline on MFMA 16x16x32. At equal cycles per FLOP the chip holds
 // a higher clock on the 16x16x32 shape than on 32x32x16 with operands re-read from LDS
@@ -745,12 +418,25 @@ __device__ __forceinline__ void mfma16_guard(f32x4 (&acc)[4][4]) {
                  "+v"(acc[2][2]), "+v"(acc[2][3]), "+v"(acc[3][0]), "+v"(acc[3][1]), "+v"(acc[3][2]),
                  "+v"(acc[3][3]));
 }
+__device__ __forceinline__ void mfma16_guard(f32x4 (&acc)[4][1]) {
+  asm volatile("s_nop 15\n\ts_nop 3" : "+v"(acc[0][0]), "+v"(acc[1][0]), "+v"(acc[2][0]), "+v"(acc[3][0]));
+}
 
-// ABL (timing only, env MRAG_SCAN_ABLATE=20+ABL): 1 = no epilogue, 4 = no epilogue, no LDS-DMA.
-// FRONT = LDS-DMA pieces of the next tile issued per k-step (1, 2 or 4): with FRONT > 1 all of
-// them go out in the first 1/FRONT of the tile, so the last piece has the rest of the tile to
-// land before the end-of-tile vmcnt(0) + barrier (FRONT 1: the last one right before that wait)
-template <int DP, int ABL = 0, int MODE = 0, int FRONT = 4>
+// The next tile's LDS-DMA pieces go out FRONT = 4 per k-step, all in the first quarter of the
+// tile, so the last piece has three quarters of the tile to land before the end-of-tile
+// vmcnt(0) + barrier (1 or 2 per k-step measured slower: notes/knn_scan_experiments.md).
+//
+// MODE 1 = the sample pre-pass: the same MFMA pipeline over a strided 1/sample_stride of each
+// split's tiles, keeping only each lane's running max per lane group (no lists, no inserts); the
+// per-(split, query, lane group) maxima go to part_s for theta_init_kernel, which seeds the
+// shared threshold with the k-th largest of them.
+//
+// QB = query blocks of 16 per wave: 4 (a workgroup holds 256 queries; the MFMA-bound batches)
+// or 1 (64 queries: the small batches of the reference's own call pattern, one query per
+// retrieve_text / retrieve_images, app/ml/retrieve.py:53,84). With one block a tile costs a
+// quarter of the MFMAs, so the scan streams the corpus at the fill / HBM rate instead of
+// padding a single query to 256 (K7s). Lists, thresholds, part_tau and outputs are the same.
+template <int DP, int MODE = 0, int QB = 4>
 __global__ __launch_bounds__(SCAN2_THREADS) void knn_scan3_kernel(ScanParams p) {
   constexpr int KSTEPS = DP / 32;
   constexpr int ROW_BYTES = DP * 2;
@@ -759,9 +445,9 @@ __global__ __launch_bounds__(SCAN2_THREADS) void knn_scan3_kernel(ScanParams p) 
   constexpr int GLDS_PER_WAVE = TILE_BYTES / 1024 / SCAN2_WAVES;
   static_assert(GLDS_PER_WAVE == KSTEPS, "one LDS-DMA piece per k-step");
   static_assert(CPR % 16 == 0, "swizzle needs rows of a multiple of 16 chunks");
-  constexpr bool NO_EPI = ABL == 1 || ABL == 4;
-  constexpr bool NO_GLDS = ABL == 4;
-  constexpr int NGROUPS = 16;  // group g: query block g >> 2, row block g & 3
+  constexpr int FRONT = 4;
+  constexpr int NGROUPS = 4 * QB;  // group g: query block g >> 2, row block g & 3
+  constexpr int QPW3 = 16 * QB, QPG3 = SCAN2_WAVES * QPW3;  // queries per wave / workgroup
   constexpr int LBL_OFF = 2 * TILE_BYTES;
   __shared__ __attribute__((aligned(16))) char smem[2 * TILE_BYTES + 2 * TILE_ROWS * 4];
 
@@ -783,31 +469,35 @@ __global__ __launch_bounds__(SCAN2_THREADS) void knn_scan3_kernel(ScanParams p) 
       split = b / p.qgroups;
     }
   }
-  // query slot of block qb is slot0 + 16 qb; Qp is a multiple of QPG so every slot exists
-  const int slot0 = qg * QPG + w * QPW2 + c16;
+  // query slot of block qb is slot0 + 16 qb; Qp is a multiple of QPG3 so every slot exists
+  const int slot0 = qg * QPG3 + w * QPW3 + c16;
 
-  half8 qf[KSTEPS][4];
+  half8 qf[KSTEPS][QB];
 #pragma unroll
   for (int kk = 0; kk < KSTEPS; ++kk)
 #pragma unroll
-    for (int qb = 0; qb < 4; ++qb)
+    for (int qb = 0; qb < QB; ++qb)
       qf[kk][qb] = *(const half8*)(p.q16 + (size_t)(slot0 + 16 * qb) * DP + kk * 32 + g4 * 8);
 #pragma unroll
   for (int kk = 0; kk < KSTEPS; ++kk)
-    asm volatile("" ::"a"(qf[kk][0]), "a"(qf[kk][1]), "a"(qf[kk][2]), "a"(qf[kk][3]));
-
-  float ls[4][KL3];
-  int li[4][KL3];
 #pragma unroll
-  for (int qb = 0; qb < 4; ++qb)
+    for (int qb = 0; qb < QB; ++qb) asm volatile("" ::"a"(qf[kk][qb]));
+
+  float ls[QB][KL3];
+  int li[QB][KL3];
+  float theta_f[QB], published[QB];
+  uint32_t theta_next[QB];
+#pragma unroll
+  for (int qb = 0; qb < QB; ++qb) {
 #pragma unroll
     for (int j = 0; j < KL3; ++j) {
       ls[qb][j] = -INFINITY;
       li[qb][j] = -1;
     }
-  float theta_f[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
-  uint32_t theta_next[4] = {0u, 0u, 0u, 0u};
-  float published[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+    theta_f[qb] = -INFINITY;
+    published[qb] = -INFINITY;
+    theta_next[qb] = 0u;
+  }
   uint32_t* const theta_q = p.theta + slot0;
   const bool may_publish = p.k <= KL3;
 
@@ -815,11 +505,11 @@ __global__ __launch_bounds__(SCAN2_THREADS) void knn_scan3_kernel(ScanParams p) 
   // offset (offA0 ^ ((kk & 3) << 6)) + (kk >> 2) * 256 + rb * 16 * ROW_BYTES
   const int offA0_init = c16 * ROW_BYTES + 16 * (g4 ^ c16);
 
-  f32x4 acc[2][4][4];  // [buffer][row block][query block]
+  f32x4 acc[2][4][QB];  // [buffer][row block][query block]
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < QB; ++j) {
       acc[1][i][j] = f32x4{-INFINITY, -INFINITY, -INFINITY, -INFINITY};
       acc[0][i][j] = f32x4{};
     }
@@ -830,7 +520,9 @@ __global__ __launch_bounds__(SCAN2_THREADS) void knn_scan3_kernel(ScanParams p) 
     my_tiles = min(my_tiles, p.sample_tiles);
     tstep = p.splits * p.sample_stride;
   }
-  float smax[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+  float smax[QB];
+#pragma unroll
+  for (int qb = 0; qb < QB; ++qb) smax[qb] = -INFINITY;
 
   auto stage_piece = [&](int buf, int tile, int i, int lane_t) {
     const char* gt = (const char*)p.x16 + (size_t)tile * TILE_BYTES;
@@ -851,26 +543,22 @@ __global__ __launch_bounds__(SCAN2_THREADS) void knn_scan3_kernel(ScanParams p) 
     constexpr int Y = decltype(y_c)::value;
     constexpr int qb = G >> 2, rb = G & 3;
     f32x4& av = acc[Y][rb][qb];
-    if constexpr (NO_EPI) {
-      asm volatile("" ::"v"(av));
+    const float gm = fmaxf(fmaxf(av[0], av[1]), fmaxf(av[2], av[3]));
+    if constexpr (MODE == 1) {
+      smax[qb] = fmaxf(smax[qb], gm);
+      asm volatile("" : "+v"(smax[qb]));
     } else {
-      const float gm = fmaxf(fmaxf(av[0], av[1]), fmaxf(av[2], av[3]));
-      if constexpr (MODE == 1) {
-        smax[qb] = fmaxf(smax[qb], gm);
-        asm volatile("" : "+v"(smax[qb]));
-      } else {
-        if (__any(gm > fmaxf(ls[qb][KL3 - 1], theta_f[qb]))) {
+      if (__any(gm > fmaxf(ls[qb][KL3 - 1], theta_f[qb]))) {
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float sv = av[r];
-            if (sv > fmaxf(ls[qb][KL3 - 1], theta_f[qb]))
-              list_insert<KL3>(ls[qb], li[qb], sv, prow + 16 * rb + r);
-          }
-          if (may_publish && li[qb][KL3 - 1] >= 0 && ls[qb][KL3 - 1] > published[qb]) {
-            published[qb] = ls[qb][KL3 - 1];
-            __hip_atomic_fetch_max(theta_q + 16 * qb, mrag_f2ord(published[qb]), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-          }
+        for (int r = 0; r < 4; ++r) {
+          const float sv = av[r];
+          if (sv > fmaxf(ls[qb][KL3 - 1], theta_f[qb]))
+            list_insert<KL3>(ls[qb], li[qb], sv, prow + 16 * rb + r);
+        }
+        if (may_publish && li[qb][KL3 - 1] >= 0 && ls[qb][KL3 - 1] > published[qb]) {
+          published[qb] = ls[qb][KL3 - 1];
+          __hip_atomic_fetch_max(theta_q + 16 * qb, mrag_f2ord(published[qb]), __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
         }
       }
     }
@@ -887,7 +575,7 @@ __global__ __launch_bounds__(SCAN2_THREADS) void knn_scan3_kernel(ScanParams p) 
     asm volatile("" : "+s"(gw), "+s"(ldsw));
     if constexpr (MODE == 0) {
 #pragma unroll
-      for (int qb = 0; qb < 4; ++qb)
+      for (int qb = 0; qb < QB; ++qb)
         theta_next[qb] = __hip_atomic_load(theta_q + 16 * qb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     const int lab = ((const int*)(smem + LBL_OFF + X * TILE_ROWS * 4))[lane];
@@ -902,7 +590,7 @@ __global__ __launch_bounds__(SCAN2_THREADS) void knn_scan3_kernel(ScanParams p) 
     // once per tile and restored before the barrier
     uint32_t m0_keep = 0;
     uint32_t voff = 0;
-    if constexpr (CPR == 64 && !NO_GLDS) asm volatile("s_mov_b32 %0, m0" : "=s"(m0_keep));
+    if constexpr (CPR == 64 && QB == 4) asm volatile("s_mov_b32 %0, m0" : "=s"(m0_keep));
     half8 a[4];
     auto read_a = [&](int kk, int rb) {
       a[rb] = *(const half8*)(tb + ((offA0 ^ ((kk & 3) << 6)) + (kk >> 2) * 256 + rb * 16 * ROW_BYTES));
@@ -910,7 +598,26 @@ __global__ __launch_bounds__(SCAN2_THREADS) void knn_scan3_kernel(ScanParams p) 
 #pragma unroll
     for (int rb = 0; rb < 4; ++rb) read_a(0, rb);
     stage_labels(Y, ntile);
-    static_for<KSTEPS>([&](auto kk_c) {
+    if constexpr (QB == 1) {
+      // K7s (fill-bound): every piece of the next tile at the top of the tile, so the DMA has the
+      // whole tile to land; per k-step the four row blocks' MFMAs, each followed by its next
+      // fragment read; the previous tile's four group tests in the first k-step's gaps
+#pragma unroll
+      for (int i = 0; i < GLDS_PER_WAVE; ++i) stage_piece(Y, ntile, i, lane_t);
+      static_for<KSTEPS>([&](auto kk_c) {
+        constexpr int kk = decltype(kk_c)::value;
+        static_for<4>([&](auto rb_c) {
+          constexpr int rb = decltype(rb_c)::value;
+          if constexpr (kk == 0)
+            mfma16_ab0(acc[X][rb][0], a[rb], qf[kk][0]);
+          else
+            mfma16_ab(acc[X][rb][0], a[rb], qf[kk][0]);
+          if constexpr (kk + 1 < KSTEPS) read_a(kk + 1, rb);
+          if constexpr (kk == 0) epi_group(std::integral_constant<int, rb>{}, std::integral_constant<int, Y>{});
+          __builtin_amdgcn_sched_barrier(0);
+        });
+      });
+    } else static_for<KSTEPS>([&](auto kk_c) {
       constexpr int kk = decltype(kk_c)::value;
       constexpr int g0 = (kk * NGROUPS + KSTEPS - 1) / KSTEPS;        // this k-step's groups:
       constexpr int g1 = ((kk + 1) * NGROUPS + KSTEPS - 1) / KSTEPS;  // [g0, g1), at most 4
@@ -926,13 +633,13 @@ __global__ __launch_bounds__(SCAN2_THREADS) void knn_scan3_kernel(ScanParams p) 
           if constexpr (kk + 1 < KSTEPS) read_a(kk + 1, rb);
         } else if constexpr ((j & 3) == 1) {  // piece FRONT kk + (j >> 2): m0 + source offset
           constexpr int pc = FRONT * kk + (j >> 2);
-          if constexpr (CPR == 64 && !NO_GLDS && (j >> 2) < FRONT && pc < GLDS_PER_WAVE) {
+          if constexpr (CPR == 64 && (j >> 2) < FRONT && pc < GLDS_PER_WAVE) {
             voff = (lane16 ^ (uint32_t)(pc << 4)) + (uint32_t)(pc * 1024);
             asm volatile("s_mov_b32 m0, %1" : "+v"(voff) : "s"(ldsw + pc * 1024));
           }
         } else if constexpr ((j & 3) == 2) {  // ... and its DMA
           constexpr int pc = FRONT * kk + (j >> 2);
-          if constexpr (!NO_GLDS && (j >> 2) < FRONT && pc < GLDS_PER_WAVE) {
+          if constexpr ((j >> 2) < FRONT && pc < GLDS_PER_WAVE) {
             if constexpr (CPR == 64)
               asm volatile("global_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(gw) : "memory");
             else
@@ -946,7 +653,7 @@ __global__ __launch_bounds__(SCAN2_THREADS) void knn_scan3_kernel(ScanParams p) 
       });
     });
     mfma16_guard(acc[X]);
-    if constexpr (CPR == 64 && !NO_GLDS) asm volatile("s_mov_b32 m0, %0" ::"s"(m0_keep));
+    if constexpr (CPR == 64 && QB == 4) asm volatile("s_mov_b32 m0, %0" ::"s"(m0_keep));
     if (tile_mask != ~0ull) {
       const uint64_t lm = tile_mask >> (4 * g4);
 #pragma unroll
@@ -955,16 +662,17 @@ __global__ __launch_bounds__(SCAN2_THREADS) void knn_scan3_kernel(ScanParams p) 
         for (int r = 0; r < 4; ++r) {
           const bool ok = (lm >> (16 * rb + r)) & 1ull;
 #pragma unroll
-          for (int qb = 0; qb < 4; ++qb) acc[X][rb][qb][r] = ok ? acc[X][rb][qb][r] : -INFINITY;
+          for (int qb = 0; qb < QB; ++qb) acc[X][rb][qb][r] = ok ? acc[X][rb][qb][r] : -INFINITY;
         }
     }
     prow = tile * TILE_ROWS + 4 * g4;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if constexpr (MODE == 0) {
 #pragma unroll
-      for (int qb = 0; qb < 4; ++qb)
+      for (int qb = 0; qb < QB; ++qb) {
         if (theta_next[qb] != 0) theta_f[qb] = fmaxf(theta_f[qb], mrag_ord2f(theta_next[qb]));
-      asm volatile("" : "+v"(theta_f[0]), "+v"(theta_f[1]), "+v"(theta_f[2]), "+v"(theta_f[3]));
+        asm volatile("" : "+v"(theta_f[qb]));
+      }
     }
     __syncthreads();
   };
@@ -988,7 +696,7 @@ __global__ __launch_bounds__(SCAN2_THREADS) void knn_scan3_kernel(ScanParams p) 
 
   if constexpr (MODE == 1) {
 #pragma unroll
-    for (int qb = 0; qb < 4; ++qb) {
+    for (int qb = 0; qb < QB; ++qb) {
       // four maxima per (split, query) over disjoint rows: lane group g4 = 0..3 (theta_init
       // takes the k-th largest of all splits' values: a valid lower bound, tighter than two)
       p.part_s[((size_t)split * p.Qp + slot0 + 16 * qb) * 4 + g4] = smax[qb];
@@ -997,631 +705,7 @@ __global__ __launch_bounds__(SCAN2_THREADS) void knn_scan3_kernel(ScanParams p) 
   }
   // fold the four lanes of each query (lanes c16 + 16 g) into one 8-list on g4 == 0
 #pragma unroll
-  for (int qb = 0; qb < 4; ++qb) {
-    float fs[8];
-    int fi[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      fs[j] = j < KL3 ? ls[qb][j] : -INFINITY;
-      fi[j] = j < KL3 ? li[qb][j] : -1;
-    }
-    float tau = li[qb][KL3 - 1] >= 0 ? ls[qb][KL3 - 1] : -INFINITY;
-#pragma unroll
-    for (int o = 16; o < 64; o += 16) {
-#pragma unroll
-      for (int j = 0; j < KL3; ++j) {
-        const float ps = __shfl_xor(ls[qb][j], o);
-        const int pi = __shfl_xor(li[qb][j], o);
-        if (pi >= 0 && ps > fs[7]) list_insert<8>(fs, fi, ps, pi);
-      }
-      const int plast = __shfl_xor(li[qb][KL3 - 1], o);
-      const float pl = __shfl_xor(ls[qb][KL3 - 1], o);
-      if (plast >= 0) tau = fmaxf(tau, pl);
-    }
-    if (g4 == 0) {
-      const int slot = slot0 + 16 * qb;
-      float* os = p.part_s + ((size_t)split * p.Qp + slot) * 8;
-      int32_t* oi = p.part_i + ((size_t)split * p.Qp + slot) * 8;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        os[j] = fs[j];
-        oi[j] = fi[j];
-      }
-      if (fi[7] >= 0) tau = fmaxf(tau, fs[7]);
-      p.part_tau[(size_t)split * p.Qp + slot] = tau;
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------
-// K7 v5 = v3 with three LDS tile buffers of 48 rows (3 x 48 KiB at DP = 512) instead of two of 64:
-// the LDS-DMA of tile t + 2 is issued in the first k-steps of tile t and stays in flight across
-// the end-of-tile barrier (counted vmcnt, raw s_barrier), so a tile's pieces have two tile
-// durations to land instead of most of one — the v3 ablations put 0.12-0.15 ms of its 0.85-0.9 ms
-// on waiting for that DMA. Lists, group tests, part_tau, threshold publishing and outputs are
-// exactly v3's; 3 row blocks of 16 per tile (12 MFMA 16x16x32 per k-step, 12 group tests per
-// tile). The index capacity is a multiple of 768 rows so 48-row tiles never leave it.
-constexpr int T5_ROWS = 48;
-constexpr int T5_RB = T5_ROWS / 16;
-constexpr int T5_NBUF = 3;
-
-__device__ __forceinline__ void mfma16_guard3(f32x4 (&acc)[T5_RB][4]) {
-  asm volatile("s_nop 15\n\ts_nop 3"
-               : "+v"(acc[0][0]), "+v"(acc[0][1]), "+v"(acc[0][2]), "+v"(acc[0][3]), "+v"(acc[1][0]),
-                 "+v"(acc[1][1]), "+v"(acc[1][2]), "+v"(acc[1][3]), "+v"(acc[2][0]), "+v"(acc[2][1]),
-                 "+v"(acc[2][2]), "+v"(acc[2][3]));
-}
-
-template <int DP, int ABL = 0, int MODE = 0, int FRONT = 3>
-__global__ __launch_bounds__(SCAN2_THREADS) void knn_scan5_kernel(ScanParams p) {
-  constexpr int KSTEPS = DP / 32;
-  constexpr int ROW_BYTES = DP * 2;
-  constexpr int TILE_BYTES = T5_ROWS * ROW_BYTES;
-  constexpr int CPR = DP / 8;
-  // a 48-row tile is 12 / 24 / 36 / 48 pieces of 1 KB (one LDS-DMA instruction each) at DP =
-  // 128 / 256 / 384 / 512: when the waves do not divide them, wave w takes pieces w, w + W, ...
-  // (GLDS_PER_WAVE or GLDS_PER_WAVE - 1 of them), otherwise a contiguous run
-  constexpr int NPIECES = TILE_BYTES / 1024;
-  constexpr bool EVEN = NPIECES % SCAN2_WAVES == 0;
-  constexpr int GLDS_PER_WAVE = (NPIECES + SCAN2_WAVES - 1) / SCAN2_WAVES;
-  static_assert(TILE_BYTES % 1024 == 0, "whole pieces");
-  static_assert(GLDS_PER_WAVE <= FRONT * KSTEPS && FRONT <= T5_RB, "the next-next tile's pieces fit the k-steps");
-  static_assert(CPR % 16 == 0, "swizzle needs rows of a multiple of 16 chunks");
-  static_assert(CPR != 64 || EVEN, "the DP = 512 DMA path assumes contiguous pieces");
-  constexpr bool NO_EPI = ABL == 1 || ABL == 4;
-  constexpr bool NO_GLDS = ABL == 4;
-  constexpr int NGROUPS = 4 * T5_RB;  // group g: query block g / T5_RB, row block g % T5_RB
-  constexpr int LBL_OFF = T5_NBUF * TILE_BYTES;
-  // shared thresholds of the workgroup's query slots, one copy per tile parity: wave w DMAs its
-  // 64 slots (lane = 16 qb + c16) into THETA_OFF + X * THETA_SET + 256 w
-  constexpr int THETA_OFF = LBL_OFF + T5_NBUF * 256;
-  constexpr int THETA_SET = SCAN2_WAVES * 256;
-  static_assert(QPW2 == 64, "one 64-slot theta row per wave");
-  constexpr uint64_t FULL = (1ull << T5_ROWS) - 1;
-  __shared__ __attribute__((aligned(16))) char smem[THETA_OFF + 2 * THETA_SET];
-
-  const int lane = threadIdx.x & 63;
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int g4 = lane >> 4;
-  const int c16 = lane & 15;
-  const uint32_t lds_base = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)((AS3 char*)smem));
-
-  int qg, split;  // same XCD-aware block mapping as v1 / v2
-  {
-    const int b = blockIdx.x;
-    if ((p.splits & 7) == 0) {
-      const int xcd = b & 7, sl = b >> 3;
-      qg = sl % p.qgroups;
-      split = (sl / p.qgroups) * 8 + xcd;
-    } else {
-      qg = b % p.qgroups;
-      split = b / p.qgroups;
-    }
-  }
-  // query slot of block qb is slot0 + 16 qb; Qp is a multiple of QPG so every slot exists
-  const int slot0 = qg * QPG + w * QPW2 + c16;
-
-  half8 qf[KSTEPS][4];
-#pragma unroll
-  for (int kk = 0; kk < KSTEPS; ++kk)
-#pragma unroll
-    for (int qb = 0; qb < 4; ++qb)
-      qf[kk][qb] = *(const half8*)(p.q16 + (size_t)(slot0 + 16 * qb) * DP + kk * 32 + g4 * 8);
-#pragma unroll
-  for (int kk = 0; kk < KSTEPS; ++kk)
-    asm volatile("" ::"a"(qf[kk][0]), "a"(qf[kk][1]), "a"(qf[kk][2]), "a"(qf[kk][3]));
-
-  float ls[4][KL3];
-  int li[4][KL3];
-#pragma unroll
-  for (int qb = 0; qb < 4; ++qb)
-#pragma unroll
-    for (int j = 0; j < KL3; ++j) {
-      ls[qb][j] = -INFINITY;
-      li[qb][j] = -1;
-    }
-  float theta_f[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
-  uint32_t theta_next[4] = {0u, 0u, 0u, 0u};
-  float published[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
-  uint32_t* const theta_q = p.theta + slot0;
-  const bool may_publish = p.k <= KL3;
-
-  // A fragment of row 16 rb + c16, chunk 4 kk + g4, sits at chunk (4 kk + g4) ^ c16: byte
-  // offset (offA0 ^ ((kk & 3) << 6)) + (kk >> 2) * 256 + rb * 16 * ROW_BYTES
-  const int offA0_init = c16 * ROW_BYTES + 16 * (g4 ^ c16);
-
-  f32x4 acc[2][T5_RB][4];  // [buffer][row block][query block]
-#pragma unroll
-  for (int i = 0; i < T5_RB; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      acc[1][i][j] = f32x4{-INFINITY, -INFINITY, -INFINITY, -INFINITY};
-      acc[0][i][j] = f32x4{};
-    }
-
-  int my_tiles = (split < p.ntiles) ? (p.ntiles - 1 - split) / p.splits + 1 : 0;
-  int tstep = p.splits;
-  if constexpr (MODE == 1) {
-    my_tiles = min(my_tiles, p.sample_tiles);
-    tstep = p.splits * p.sample_stride;
-  }
-  float smax[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
-
-  const int my_pieces = EVEN ? GLDS_PER_WAVE : (NPIECES - w + SCAN2_WAVES - 1) / SCAN2_WAVES;  // wave-uniform
-  auto stage_piece = [&](int buf, int tile, int i, int lane_t) {
-    const char* gt = (const char*)p.x16 + (size_t)tile * TILE_BYTES;
-    const unsigned piece = EVEN ? w * GLDS_PER_WAVE + i : i * SCAN2_WAVES + w;
-    const unsigned P = piece * 64 + (unsigned)lane_t;
-    const unsigned row = P / CPR;
-    const unsigned pos = P - row * CPR;
-    const unsigned c = pos ^ (row & 15);
-    glds_x4(gt + row * ROW_BYTES + c * 16, lds_base + buf * TILE_BYTES + piece * 1024);
-  };
-  auto stage_labels = [&](int buf, int tile) {  // lanes >= T5_ROWS would read the next tile's labels: off
-    if (w == 0 && lane < T5_ROWS) glds_x1(p.labels + (size_t)tile * T5_ROWS + lane, lds_base + LBL_OFF + buf * 256);
-  };
-
-  int prow = 0;  // first row of the filtered tile + 4 g4
-  auto epi_group = [&](auto g_c, auto y_c) {
-    constexpr int G = decltype(g_c)::value;
-    constexpr int Y = decltype(y_c)::value;
-    constexpr int qb = G / T5_RB, rb = G % T5_RB;
-    f32x4& av = acc[Y][rb][qb];
-    if constexpr (NO_EPI) {
-      asm volatile("" ::"v"(av));
-    } else {
-      const float gm = fmaxf(fmaxf(av[0], av[1]), fmaxf(av[2], av[3]));
-      if constexpr (MODE == 1) {
-        smax[qb] = fmaxf(smax[qb], gm);
-        asm volatile("" : "+v"(smax[qb]));
-      } else {
-        if (__any(gm > fmaxf(ls[qb][KL3 - 1], theta_f[qb]))) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float sv = av[r];
-            if (sv > fmaxf(ls[qb][KL3 - 1], theta_f[qb]))
-              list_insert<KL3>(ls[qb], li[qb], sv, prow + 16 * rb + r);
-          }
-          if (may_publish && li[qb][KL3 - 1] >= 0 && ls[qb][KL3 - 1] > published[qb]) {
-            published[qb] = ls[qb][KL3 - 1];
-            __hip_atomic_fetch_max(theta_q + 16 * qb, mrag_f2ord(published[qb]), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-          }
-        }
-      }
-    }
-  };
-
-  // accumulator buffer X = it & 1 (compile time), LDS tile buffer it % 3; the DMA of tile it + 2
-  // goes into buffer (it + 2) % 3, which held tile it - 1 (every wave is past it: barrier)
-  auto tile_body = [&](auto x_c, int it) {
-    constexpr int X = decltype(x_c)::value;
-    constexpr int Y = 1 - X;
-    const int tile = split + it * tstep;
-    const bool has_nn = it + 2 < my_tiles;  // wave-uniform
-    const int ntile = tile + 2 * tstep;
-    const int bi = it % T5_NBUF, bn = (it + 2) % T5_NBUF;
-    const char* gw = (const char*)p.x16 + (size_t)ntile * TILE_BYTES + (size_t)w * GLDS_PER_WAVE * ROW_BYTES;
-    uint32_t ldsw = lds_base + bn * TILE_BYTES + w * GLDS_PER_WAVE * 1024;
-    asm volatile("" : "+s"(gw), "+s"(ldsw));
-    if constexpr (MODE == 0) {
-      // the thresholds travel by LDS-DMA, not into registers: a register loaded by inline asm is
-      // "ready" to the compiler at once, and it may copy it (before the wait) into the register
-      // the consumer wants — that read a stale threshold of another query block. The DMA is older
-      // than this tile's pieces, so the end-of-tile vmcnt(N) retires it (no drain of the ring);
-      // a stale value is a threshold that once held, hence still a valid lower bound
-      glds_x1(theta_q - c16 + lane, lds_base + THETA_OFF + X * THETA_SET + w * 256);
-    }
-    const int lab = ((const int*)(smem + LBL_OFF + bi * 256))[lane];
-    const bool lab_ok = lane < T5_ROWS && ((p.label_filter == MRAG_LABEL_ANY) ? (lab >= 0) : (lab == p.label_filter));
-    const uint64_t tile_mask = __ballot(lab_ok);
-    const char* tb = smem + bi * TILE_BYTES;
-    int lane_t = lane, offA0 = offA0_init;
-    uint32_t lane16 = lane * 16;
-    asm volatile("" : "+v"(lane_t), "+v"(offA0), "+v"(lane16));
-    // DP = 512: m0 holds the piece's LDS address from gap 1 to the DMA in gap 2 (nothing the
-    // compiler emits in this loop reads m0: ds_read_b128 / MFMA / VALU / SALU only); it is saved
-    // once per tile and restored before the barrier
-    uint32_t m0_keep = 0;
-    uint32_t voff = 0;
-    if constexpr (CPR == 64 && !NO_GLDS) asm volatile("s_mov_b32 %0, m0" : "=s"(m0_keep));
-    half8 a[T5_RB];
-    const uint32_t rw = (uint32_t)(GLDS_PER_WAVE * w);  // first tile row of this wave's pieces (DP = 512)
-    auto read_a = [&](int kk, int rb) {
-      a[rb] = *(const half8*)(tb + ((offA0 ^ ((kk & 3) << 6)) + (kk >> 2) * 256 + rb * 16 * ROW_BYTES));
-    };
-#pragma unroll
-    for (int rb = 0; rb < T5_RB; ++rb) read_a(0, rb);
-    if (has_nn) stage_labels(bn, ntile);
-    static_for<KSTEPS>([&](auto kk_c) {
-      constexpr int kk = decltype(kk_c)::value;
-      constexpr int g0 = (kk * NGROUPS + KSTEPS - 1) / KSTEPS;        // this k-step's groups:
-      constexpr int g1 = ((kk + 1) * NGROUPS + KSTEPS - 1) / KSTEPS;  // [g0, g1), at most 4
-      static_for<4 * T5_RB>([&](auto j_c) {
-        constexpr int j = decltype(j_c)::value;
-        constexpr int rb = j >> 2, qb = j & 3;
-        if constexpr (kk == 0)
-          mfma16_ab0(acc[X][rb][qb], a[rb], qf[kk][qb]);
-        else
-          mfma16_ab(acc[X][rb][qb], a[rb], qf[kk][qb]);
-        // one job per MFMA gap
-        if constexpr ((j & 3) == 3) {  // after the last MFMA of block rb: its next fragment
-          if constexpr (kk + 1 < KSTEPS) read_a(kk + 1, rb);
-        } else if constexpr ((j & 3) == 1) {  // piece FRONT kk + (j >> 2): m0 + source offset
-          constexpr int pc = FRONT * kk + (j >> 2);
-          if constexpr (CPR == 64 && !NO_GLDS && (j >> 2) < FRONT && pc < GLDS_PER_WAVE) {
-            voff = (lane16 ^ (((rw + pc) & 15u) << 4)) + (uint32_t)(pc * 1024);
-            asm volatile("s_mov_b32 m0, %1" : "+v"(voff) : "s"(ldsw + pc * 1024));
-          }
-        } else if constexpr ((j & 3) == 2) {  // ... and its DMA
-          constexpr int pc = FRONT * kk + (j >> 2);
-          if constexpr (!NO_GLDS && (j >> 2) < FRONT && pc < GLDS_PER_WAVE) {
-            if (has_nn) {
-              if constexpr (CPR == 64)
-                asm volatile("global_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(gw) : "memory");
-              else if (EVEN || pc < my_pieces)
-                stage_piece(bn, ntile, pc, lane_t);
-            }
-          }
-        } else if constexpr ((j & 3) == 0) {
-          if constexpr (g0 + (j >> 2) < g1)
-            epi_group(std::integral_constant<int, g0 + (j >> 2)>{}, std::integral_constant<int, Y>{});
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      });
-    });
-    mfma16_guard3(acc[X]);
-    if constexpr (CPR == 64 && !NO_GLDS) asm volatile("s_mov_b32 m0, %0" ::"s"(m0_keep));
-    if (tile_mask != FULL) {
-      const uint64_t lm = tile_mask >> (4 * g4);
-#pragma unroll
-      for (int rb = 0; rb < T5_RB; ++rb)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const bool ok = (lm >> (16 * rb + r)) & 1ull;
-#pragma unroll
-          for (int qb = 0; qb < 4; ++qb) acc[X][rb][qb][r] = ok ? acc[X][rb][qb][r] : -INFINITY;
-        }
-    }
-    prow = tile * T5_ROWS + 4 * g4;
-    // tile it + 1 (DMA issued during tile it - 1) must have landed; tile it + 2's pieces (the
-    // youngest GLDS_PER_WAVE operations of this wave) stay in flight across the barrier
-    if (has_nn && (EVEN || my_pieces == GLDS_PER_WAVE)) {
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GLDS_PER_WAVE) : "memory");
-    } else if (!EVEN && has_nn) {
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(EVEN ? GLDS_PER_WAVE : GLDS_PER_WAVE - 1) : "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    if constexpr (MODE == 0) {
-      // this wave's own DMA, retired by its vmcnt: no barrier needed; slot X is rewritten two
-      // tiles later, after the lgkmcnt(0) below has returned this read
-      const uint32_t* th = (const uint32_t*)(smem + THETA_OFF + X * THETA_SET + w * 256);
-#pragma unroll
-      for (int qb = 0; qb < 4; ++qb) theta_next[qb] = th[16 * qb + c16];
-#pragma unroll
-      for (int qb = 0; qb < 4; ++qb)
-        if (theta_next[qb] != 0) theta_f[qb] = fmaxf(theta_f[qb], mrag_ord2f(theta_next[qb]));
-      asm volatile("" : "+v"(theta_f[0]), "+v"(theta_f[1]), "+v"(theta_f[2]), "+v"(theta_f[3]));
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    // the barrier intrinsic is not a memory operation to LLVM: without this compiler fence the
-    // next tile's LDS reads (labels, A fragments) may be hoisted above it (MODE 1 has no other
-    // memory-clobbering statement in between) and read a buffer before its DMA has landed
-    asm volatile("" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-  };
-
-  if (my_tiles > 0) {
-    // prologue: tiles 0 and 1 into buffers 0 and 1, landed before the first read
-#pragma unroll
-    for (int i = 0; i < GLDS_PER_WAVE; ++i)
-      if (i < my_pieces) stage_piece(0, split, i, lane);
-    stage_labels(0, split);
-    if (my_tiles > 1) {
-#pragma unroll
-      for (int i = 0; i < GLDS_PER_WAVE; ++i)
-        if (i < my_pieces) stage_piece(1, split + tstep, i, lane);
-      stage_labels(1, split + tstep);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    for (int it = 0; it < my_tiles; it += 2) {
-      tile_body(std::integral_constant<int, 0>{}, it);
-      if (it + 1 < my_tiles) tile_body(std::integral_constant<int, 1>{}, it + 1);
-    }
-    if (my_tiles & 1) {
-      static_for<NGROUPS>([&](auto g_c) { epi_group(g_c, std::integral_constant<int, 0>{}); });
-    } else {
-      static_for<NGROUPS>([&](auto g_c) { epi_group(g_c, std::integral_constant<int, 1>{}); });
-    }
-  }
-
-  if constexpr (MODE == 1) {
-    // two maxima per (split, query) over disjoint rows: lane groups {0, 1} and {2, 3}
-#pragma unroll
-    for (int qb = 0; qb < 4; ++qb) {
-      const float m = fmaxf(smax[qb], __shfl_xor(smax[qb], 16));
-      if ((g4 & 1) == 0) p.part_s[((size_t)split * p.Qp + slot0 + 16 * qb) * 2 + (g4 >> 1)] = m;
-    }
-    return;
-  }
-  // fold the four lanes of each query (lanes c16 + 16 g) into one 8-list on g4 == 0
-#pragma unroll
-  for (int qb = 0; qb < 4; ++qb) {
-    float fs[8];
-    int fi[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      fs[j] = j < KL3 ? ls[qb][j] : -INFINITY;
-      fi[j] = j < KL3 ? li[qb][j] : -1;
-    }
-    float tau = li[qb][KL3 - 1] >= 0 ? ls[qb][KL3 - 1] : -INFINITY;
-#pragma unroll
-    for (int o = 16; o < 64; o += 16) {
-#pragma unroll
-      for (int j = 0; j < KL3; ++j) {
-        const float ps = __shfl_xor(ls[qb][j], o);
-        const int pi = __shfl_xor(li[qb][j], o);
-        if (pi >= 0 && ps > fs[7]) list_insert<8>(fs, fi, ps, pi);
-      }
-      const int plast = __shfl_xor(li[qb][KL3 - 1], o);
-      const float pl = __shfl_xor(ls[qb][KL3 - 1], o);
-      if (plast >= 0) tau = fmaxf(tau, pl);
-    }
-    if (g4 == 0) {
-      const int slot = slot0 + 16 * qb;
-      float* os = p.part_s + ((size_t)split * p.Qp + slot) * 8;
-      int32_t* oi = p.part_i + ((size_t)split * p.Qp + slot) * 8;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        os[j] = fs[j];
-        oi[j] = fi[j];
-      }
-      if (fi[7] >= 0) tau = fmaxf(tau, fs[7]);
-      p.part_tau[(size_t)split * p.Qp + slot] = tau;
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------
-// K7 v4 (top-k mode and sample pre-pass; same lists, part_tau and outputs as v3): two waves per
-// SIMD instead of one, so one wave's MFMAs cover its sibling's LDS-DMA issue, end-of-tile
-// waits, barriers and filter work.
-//  * one workgroup = 8 waves = 256 queries x one split; a wave owns 32 queries as two 16-query
-//    blocks whose B fragments (DP/4 registers: 128 AGPRs at DP = 512) stay in AGPRs, leaving
-//    the other half of a 256-register wave for single-buffered accumulators, one A-fragment
-//    set and the lane lists (KL3 = 6, as v3);
-//  * a 64-row tile is processed in two phases of KSTEPS/2 k-steps (8 MFMA 16x16x32 per k-step:
-//    4 row blocks x 2 query blocks), each phase ended by a raw s_barrier; waves 4..7 (group B,
-//    one per SIMD beside a wave of group A) run one barrier behind waves 0..3, so the two waves
-//    of a SIMD are always in different phases;
-//  * next-tile LDS-DMA: group B issues its pieces in phase 0 of tile t, group A in phase 1 (one
-//    per k-step), each group retiring its own with vmcnt(0) before the barrier that ends the
-//    issuing phase. With the one-barrier stagger, every wave has finished tile t - 1 (whose
-//    buffer is being refilled) before either group's issue phase starts, and every piece of
-//    tile t + 1 has landed at a barrier each wave passes before its first read of it;
-//  * the tile's group tests / list insertions run after the phase-1 MFMAs, while the sibling
-//    wave is in the middle of its own phase.
-constexpr int SCAN4_WAVES = 8;
-constexpr int SCAN4_THREADS = SCAN4_WAVES * 64;
-constexpr int QPW4 = 32;
-static_assert(SCAN4_WAVES * QPW4 == QPG, "v4 keeps the query-group size of v1");
-
-__device__ __forceinline__ void mfma16_guard8(f32x4 (&acc)[4][2]) {
-  asm volatile("s_nop 15\n\ts_nop 3"
-               : "+v"(acc[0][0]), "+v"(acc[0][1]), "+v"(acc[1][0]), "+v"(acc[1][1]), "+v"(acc[2][0]),
-                 "+v"(acc[2][1]), "+v"(acc[3][0]), "+v"(acc[3][1]));
-}
-
-template <int DP, int MODE = 0, int PPK = 4>  // PPK: DMA pieces per k-step, front-loaded in the issue phase
-__global__ __launch_bounds__(SCAN4_THREADS) void knn_scan4_kernel(ScanParams p) {
-  constexpr int KSTEPS = DP / 32;
-  constexpr int HALF = KSTEPS / 2;
-  constexpr int ROW_BYTES = DP * 2;
-  constexpr int TILE_BYTES = TILE_ROWS * ROW_BYTES;
-  constexpr int CPR = DP / 8;
-  constexpr int PIECES = TILE_BYTES / 1024 / SCAN4_WAVES;  // per wave per tile (DP / 64)
-  static_assert(KSTEPS % 2 == 0 && PIECES <= HALF * PPK && PPK <= 4, "the issue phase holds every DMA piece");
-  static_assert(CPR % 16 == 0, "swizzle needs rows of a multiple of 16 chunks");
-  constexpr int LBL_OFF = 2 * TILE_BYTES;
-  __shared__ __attribute__((aligned(16))) char smem[2 * TILE_BYTES + 2 * TILE_ROWS * 4];
-
-  const int lane = threadIdx.x & 63;
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int grp = w >> 2;  // 0: waves 0..3 (group A), 1: waves 4..7 (group B, one barrier behind)
-  const int g4 = lane >> 4;
-  const int c16 = lane & 15;
-  const uint32_t lds_base = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)((AS3 char*)smem));
-
-  int qg, split;  // same XCD-aware block mapping as v1..v3
-  {
-    const int b = blockIdx.x;
-    if ((p.splits & 7) == 0) {
-      const int xcd = b & 7, sl = b >> 3;
-      qg = sl % p.qgroups;
-      split = (sl / p.qgroups) * 8 + xcd;
-    } else {
-      qg = b % p.qgroups;
-      split = b / p.qgroups;
-    }
-  }
-  const int slot0 = qg * QPG + w * QPW4 + c16;  // query block qb: slot0 + 16 qb
-
-  half8 qf[KSTEPS][2];
-#pragma unroll
-  for (int kk = 0; kk < KSTEPS; ++kk)
-#pragma unroll
-    for (int qb = 0; qb < 2; ++qb)
-      qf[kk][qb] = *(const half8*)(p.q16 + (size_t)(slot0 + 16 * qb) * DP + kk * 32 + g4 * 8);
-#pragma unroll
-  for (int kk = 0; kk < KSTEPS; ++kk) asm volatile("" ::"a"(qf[kk][0]), "a"(qf[kk][1]));
-
-  float ls[2][KL3];
-  int li[2][KL3];
-#pragma unroll
-  for (int qb = 0; qb < 2; ++qb)
-#pragma unroll
-    for (int j = 0; j < KL3; ++j) {
-      ls[qb][j] = -INFINITY;
-      li[qb][j] = -1;
-    }
-  float theta_f[2] = {-INFINITY, -INFINITY};
-  uint32_t theta_next[2] = {0u, 0u};
-  float published[2] = {-INFINITY, -INFINITY};
-  float smax[2] = {-INFINITY, -INFINITY};
-  uint32_t* const theta_q = p.theta + slot0;
-  const bool may_publish = p.k <= KL3;
-  const int offA0 = c16 * ROW_BYTES + 16 * (g4 ^ c16);
-
-  int my_tiles = (split < p.ntiles) ? (p.ntiles - 1 - split) / p.splits + 1 : 0;
-  int tstep = p.splits;
-  if constexpr (MODE == 1) {
-    my_tiles = min(my_tiles, p.sample_tiles);
-    tstep = p.splits * p.sample_stride;
-  }
-  if (my_tiles == 0) return;  // whole workgroup, before any barrier
-
-  auto stage_piece = [&](int buf, int tile, int i) {
-    const char* gt = (const char*)p.x16 + (size_t)tile * TILE_BYTES;
-    const unsigned piece = w * PIECES + i;
-    const unsigned P = piece * 64 + (unsigned)lane;
-    const unsigned row = P / CPR;
-    const unsigned pos = P - row * CPR;
-    const unsigned c = pos ^ (row & 15);
-    glds_x4(gt + row * ROW_BYTES + c * 16, lds_base + buf * TILE_BYTES + piece * 1024);
-  };
-  auto bar = [&]() {
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");  // compiler fence: LDS reads stay after the barrier
-    __builtin_amdgcn_sched_barrier(0);
-  };
-
-  // prologue: tile 0 by every wave, landed before anyone reads it
-#pragma unroll
-  for (int i = 0; i < PIECES; ++i) stage_piece(0, split, i);
-  if (w == 0) glds_x1(p.labels + (size_t)split * TILE_ROWS + lane, lds_base + LBL_OFF);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  bar();
-  if (grp == 1) bar();
-
-  f32x4 acc[4][2];
-  half8 a[4];
-  for (int it = 0; it < my_tiles; ++it) {
-    const int X = it & 1;
-    const int tile = split + it * tstep;
-    const bool has_next = it + 1 < my_tiles;
-    const int ntile = tile + tstep;
-    if constexpr (MODE == 0) {
-#pragma unroll
-      for (int qb = 0; qb < 2; ++qb)
-        theta_next[qb] = __hip_atomic_load(theta_q + 16 * qb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    const int lab = ((const int*)(smem + LBL_OFF + X * TILE_ROWS * 4))[lane];
-    const bool lab_ok = (p.label_filter == MRAG_LABEL_ANY) ? (lab >= 0) : (lab == p.label_filter);
-    const uint64_t tile_mask = __ballot(lab_ok);
-    const char* tb = smem + X * TILE_BYTES;
-    auto read_a = [&](int kk, int rb) {
-      a[rb] = *(const half8*)(tb + ((offA0 ^ ((kk & 3) << 6)) + (kk >> 2) * 256 + rb * 16 * ROW_BYTES));
-    };
-#pragma unroll
-    for (int rb = 0; rb < 4; ++rb) read_a(0, rb);
-    auto kstep = [&](auto kk_c, bool issue) {
-      constexpr int kk = decltype(kk_c)::value;
-      constexpr int pc0 = (kk % HALF) * PPK;  // first piece issued in this k-step of the issue phase
-#pragma unroll
-      for (int rb = 0; rb < 4; ++rb) {
-        if constexpr (kk == 0) {
-          mfma16_ab0(acc[rb][0], a[rb], qf[kk][0]);
-          mfma16_ab0(acc[rb][1], a[rb], qf[kk][1]);
-        } else {
-          mfma16_ab(acc[rb][0], a[rb], qf[kk][0]);
-          mfma16_ab(acc[rb][1], a[rb], qf[kk][1]);
-        }
-        if constexpr (kk + 1 < KSTEPS) read_a(kk + 1, rb);
-        if (rb < PPK && pc0 + rb < PIECES && issue) {
-          if constexpr (CPR == 64) {  // DP = 512: a piece is one row; SGPR row base + one VALU offset
-            const int pc = pc0 + rb, row = 8 * w + pc;
-            const char* gw = (const char*)p.x16 + (size_t)ntile * TILE_BYTES + (size_t)(8 * w) * ROW_BYTES;
-            const uint32_t voff = ((uint32_t)lane ^ (uint32_t)(row & 15)) * 16u + (uint32_t)(pc * 1024);
-            glds_x4_saddr(voff, gw, lds_base + (uint32_t)((X ^ 1) * TILE_BYTES + row * 1024));
-          } else {
-            stage_piece(X ^ 1, ntile, pc0 + rb);
-          }
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    };
-    // phase 0: group B issues its pieces of the next tile
-    static_for<HALF>([&](auto kk_c) { kstep(kk_c, grp == 1 && has_next); });
-    if (grp == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    bar();
-    // phase 1: group A issues its pieces (and the labels) of the next tile
-    if (grp == 0 && w == 0 && has_next)
-      glds_x1(p.labels + (size_t)ntile * TILE_ROWS + lane, lds_base + LBL_OFF + (X ^ 1) * TILE_ROWS * 4);
-    static_for<HALF>([&](auto kk_c) {
-      kstep(std::integral_constant<int, decltype(kk_c)::value + HALF>{}, grp == 0 && has_next);
-    });
-    mfma16_guard8(acc);
-    if (tile_mask != ~0ull) {
-      const uint64_t lm = tile_mask >> (4 * g4);
-#pragma unroll
-      for (int rb = 0; rb < 4; ++rb)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const bool ok = (lm >> (16 * rb + r)) & 1ull;
-          acc[rb][0][r] = ok ? acc[rb][0][r] : -INFINITY;
-          acc[rb][1][r] = ok ? acc[rb][1][r] : -INFINITY;
-        }
-    }
-    const int prow = tile * TILE_ROWS + 4 * g4;
-#pragma unroll
-    for (int qb = 0; qb < 2; ++qb)
-#pragma unroll
-      for (int rb = 0; rb < 4; ++rb) {
-        const f32x4& av = acc[rb][qb];
-        const float gm = fmaxf(fmaxf(av[0], av[1]), fmaxf(av[2], av[3]));
-        if constexpr (MODE == 1) {
-          smax[qb] = fmaxf(smax[qb], gm);
-        } else {
-          if (__any(gm > fmaxf(ls[qb][KL3 - 1], theta_f[qb]))) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const float sv = av[r];
-              if (sv > fmaxf(ls[qb][KL3 - 1], theta_f[qb])) list_insert<KL3>(ls[qb], li[qb], sv, prow + 16 * rb + r);
-            }
-            if (may_publish && li[qb][KL3 - 1] >= 0 && ls[qb][KL3 - 1] > published[qb]) {
-              published[qb] = ls[qb][KL3 - 1];
-              __hip_atomic_fetch_max(theta_q + 16 * qb, mrag_f2ord(published[qb]), __ATOMIC_RELAXED,
-                                     __HIP_MEMORY_SCOPE_AGENT);
-            }
-          }
-        }
-      }
-    if constexpr (MODE == 0) {
-#pragma unroll
-      for (int qb = 0; qb < 2; ++qb)
-        if (theta_next[qb] != 0) theta_f[qb] = fmaxf(theta_f[qb], mrag_ord2f(theta_next[qb]));
-    }
-    if (grp == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    bar();
-  }
-  if (grp == 0) bar();  // same barrier count for both groups
-
-  if constexpr (MODE == 1) {
-#pragma unroll
-    for (int qb = 0; qb < 2; ++qb) {
-      const float m = fmaxf(smax[qb], __shfl_xor(smax[qb], 16));
-      if ((g4 & 1) == 0) p.part_s[((size_t)split * p.Qp + slot0 + 16 * qb) * 2 + (g4 >> 1)] = m;
-    }
-    return;
-  }
-  // fold the four lanes of each query (lanes c16 + 16 g) into one 8-list on g4 == 0 (as v3)
-#pragma unroll
-  for (int qb = 0; qb < 2; ++qb) {
+  for (int qb = 0; qb < QB; ++qb) {
     float fs[8];
     int fi[8];
 #pragma unroll
@@ -1658,36 +742,27 @@ __global__ __launch_bounds__(SCAN4_THREADS) void knn_scan4_kernel(ScanParams p) 
 }
 
 // Seed of the shared threshold from the sample pre-pass: per query, the k-th largest of the
-// 2*splits sample maxima (maxima of disjoint row sets, so k distinct rows score at least
+// 4*splits sample maxima (maxima of disjoint row sets, so k distinct rows score at least
 // that), lowered by a margin of 2.5 EPS so that a seed equal to the k-th best approximate
 // score cannot cost the certificate (K8 includes the final threshold in T). One wave per
 // query; k rounds of wave arg-max extraction.
 constexpr float THETA_SEED_MARGIN = (float)(2.5 * EPS_F16);
 __global__ __launch_bounds__(64) void theta_init_kernel(const float* __restrict__ smax, int nvals, int Qp, int k,
-                                                        uint32_t* __restrict__ theta, int per) {
-  constexpr int PER_LANE = 16;  // nvals = per * splits <= 4 * 256
+                                                        uint32_t* __restrict__ theta) {
+  constexpr int PER_LANE = 16;  // nvals = 4 * splits <= 4 * 256
   const int q = blockIdx.x, lane = threadIdx.x;
   float v[PER_LANE];
-  // lane l takes splits l, l + 64, ... whole (one 16-byte load for per = 4, 8 bytes for per = 2):
-  // the (split, query) groups are Qp * per floats apart, so per-value loads touched a line each;
-  // the k-th largest does not depend on which lane holds a value
-  const int splits = nvals / per;
+  // lane l takes splits l, l + 64, ... whole (one 16-byte load of the split's four maxima): the
+  // (split, query) groups are 4 Qp floats apart, so per-value loads touched a line each; the
+  // k-th largest does not depend on which lane holds a value
+  const int splits = nvals / 4;
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
     const int sp = lane + 64 * t;
-    const float* src = smax + ((size_t)sp * Qp + q) * per;
-    if (per == 4) {
-      const f32x4 x = sp < splits ? *(const f32x4*)src : f32x4{-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+    const f32x4 x = sp < splits ? *(const f32x4*)(smax + ((size_t)sp * Qp + q) * 4)
+                                : f32x4{-INFINITY, -INFINITY, -INFINITY, -INFINITY};
 #pragma unroll
-      for (int u = 0; u < 4; ++u) v[4 * t + u] = x[u];
-    } else {
-      typedef float f32x2 __attribute__((ext_vector_type(2)));
-      const f32x2 x = sp < splits ? *(const f32x2*)src : f32x2{-INFINITY, -INFINITY};
-      v[4 * t] = x[0];
-      v[4 * t + 1] = x[1];
-      v[4 * t + 2] = -INFINITY;
-      v[4 * t + 3] = -INFINITY;
-    }
+    for (int u = 0; u < 4; ++u) v[4 * t + u] = x[u];
   }
   float kth = -INFINITY;
   for (int r = 0; r < k; ++r) {
@@ -2283,60 +1358,26 @@ int kl_for(int k, int DP) {
   return 32;
 }
 
-scan_fn get_scan2(int DP, bool sample = false) {
+template <int QB>
+scan_fn get_scan3q(int DP, bool sample) {
   switch (DP) {
-    case 128: return sample ? knn_scan2_kernel<128, 0, 1> : knn_scan2_kernel<128>;
-    case 256: return sample ? knn_scan2_kernel<256, 0, 1> : knn_scan2_kernel<256>;
-    case 384: return sample ? knn_scan2_kernel<384, 0, 1> : knn_scan2_kernel<384>;
-    case 512: return sample ? knn_scan2_kernel<512, 0, 1> : knn_scan2_kernel<512>;
+    case 128: return sample ? knn_scan3_kernel<128, 1, QB> : knn_scan3_kernel<128, 0, QB>;
+    case 256: return sample ? knn_scan3_kernel<256, 1, QB> : knn_scan3_kernel<256, 0, QB>;
+    case 384: return sample ? knn_scan3_kernel<384, 1, QB> : knn_scan3_kernel<384, 0, QB>;
+    case 512: return sample ? knn_scan3_kernel<512, 1, QB> : knn_scan3_kernel<512, 0, QB>;
     default: return nullptr;
   }
 }
+scan_fn get_scan3(int DP, bool sample, int qb) { return qb == 1 ? get_scan3q<1>(DP, sample) : get_scan3q<4>(DP, sample); }
 
-scan_fn get_scan3(int DP, bool sample = false) {
-  switch (DP) {
-    case 128: return sample ? knn_scan3_kernel<128, 0, 1> : knn_scan3_kernel<128>;
-    case 256: return sample ? knn_scan3_kernel<256, 0, 1> : knn_scan3_kernel<256>;
-    case 384: return sample ? knn_scan3_kernel<384, 0, 1> : knn_scan3_kernel<384>;
-    case 512: {
-      static const int front = [] {  // env MRAG_SCAN_FRONT=1/2: DMA pieces per k-step (A/B timing)
-        const char* e = getenv("MRAG_SCAN_FRONT");
-        return e ? atoi(e) : 4;
-      }();
-      if (front == 1) return sample ? knn_scan3_kernel<512, 0, 1, 1> : knn_scan3_kernel<512, 0, 0, 1>;
-      if (front == 2) return sample ? knn_scan3_kernel<512, 0, 1, 2> : knn_scan3_kernel<512, 0, 0, 2>;
-      return sample ? knn_scan3_kernel<512, 0, 1> : knn_scan3_kernel<512>;
-    }
-    default: return nullptr;
-  }
-}
-
-scan_fn get_scan5(int DP, bool sample = false) {
-  switch (DP) {
-    case 128: return sample ? knn_scan5_kernel<128, 0, 1> : knn_scan5_kernel<128>;
-    case 256: return sample ? knn_scan5_kernel<256, 0, 1> : knn_scan5_kernel<256>;
-    case 384: return sample ? knn_scan5_kernel<384, 0, 1> : knn_scan5_kernel<384>;
-    case 512: return sample ? knn_scan5_kernel<512, 0, 1> : knn_scan5_kernel<512>;
-    default: return nullptr;
-  }
-}
-
-scan_fn get_scan4(int DP, bool sample = false) {
-  switch (DP) {
-    case 128: return sample ? knn_scan4_kernel<128, 1> : knn_scan4_kernel<128>;
-    case 256: return sample ? knn_scan4_kernel<256, 1> : knn_scan4_kernel<256>;
-    case 384: return sample ? knn_scan4_kernel<384, 1> : knn_scan4_kernel<384>;
-    case 512: {
-      static const int ppk = [] {  // env MRAG_SCAN4_PPK=1/2/4: DMA pieces per k-step (A/B timing)
-        const char* e = getenv("MRAG_SCAN4_PPK");
-        return e ? atoi(e) : 4;
-      }();
-      if (ppk == 1) return sample ? knn_scan4_kernel<512, 1, 1> : knn_scan4_kernel<512, 0, 1>;
-      if (ppk == 2) return sample ? knn_scan4_kernel<512, 1, 2> : knn_scan4_kernel<512, 0, 2>;
-      return sample ? knn_scan4_kernel<512, 1> : knn_scan4_kernel<512>;
-    }
-    default: return nullptr;
-  }
+// Query blocks per wave of the v3 scan for a batch: 1 (K7s, 64 queries per workgroup) while the
+// padded batch fits one small group, else 4 (256 per workgroup).
+int scan3_qb(int64_t nq) {
+  static const int small_max = [] {  // env MRAG_SCAN_SMALLQ (experiment): largest batch on K7s
+    const char* e = getenv("MRAG_SCAN_SMALLQ");
+    return e ? atoi(e) : 64;
+  }();
+  return nq <= small_max ? 1 : 4;
 }
 
 scan_fn get_scan(int DP, int KL, bool collect) {
@@ -2367,6 +1408,7 @@ struct SearchCtx {
   DevBuf out_s, out_s64, out_r, theta, part_tau;
   int32_t* host_counters = nullptr;  // pinned [2]: fail_cnt, overflow
   hipEvent_t done = nullptr;         // end of the search's device work (waited by spinning)
+  hipEvent_t null_ev = nullptr;      // device inputs on the NULL stream: the search waits for it
   hipEvent_t ev0 = nullptr, ev1 = nullptr;  // scan timing (mrag_knn_profile)
   mrag_knn::Workspace gws[8];               // K7g buffers
 };
@@ -2382,12 +1424,6 @@ struct mrag_knn_index {
   DevBuf stage_rows, stage_labels, rowlist;  // mutation staging
   std::mutex pool_mu;                        // guards the context pool and the stats below
   std::vector<SearchCtx*> ctx_all, ctx_free;
-  int ablate = 0;  // diagnostic knob, env MRAG_SCAN_ABLATE (timing experiments only)
-  bool scan_v1 = false;  // env MRAG_SCAN_V1=1: force the v1 top-k scan (A/B timing)
-  bool no_sample = false;  // env MRAG_SCAN_NO_SAMPLE=1: skip the threshold pre-pass (A/B timing)
-  bool scan_v2 = false;    // env MRAG_SCAN_V2=1: the 32x32x16 v2 scan instead of v3 (A/B timing)
-  bool scan_v4 = false;    // env MRAG_SCAN_V4=1: the two-waves-per-SIMD v4 scan instead of v3 (A/B timing)
-  bool scan_v5 = false;    // env MRAG_SCAN_V5=1: the three-buffer 48-row v5 scan instead of v3
   int64_t last_uncertified = 0, last_retries = 0;
   // optional scan timing (mrag_knn_profile)
   bool profile = false;
@@ -2419,6 +1455,7 @@ void ctx_free_all(SearchCtx* c) {
   mrag_knn::release(c->gws);
   if (c->host_counters) (void)hipHostFree(c->host_counters);
   if (c->done) (void)hipEventDestroy(c->done);
+  if (c->null_ev) (void)hipEventDestroy(c->null_ev);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   delete c;
@@ -2437,6 +1474,7 @@ int ctx_get(mrag_knn_index* ix, SearchCtx** out) {
   auto* c = new SearchCtx();
   hipError_t e = hipHostMalloc((void**)&c->host_counters, 16, hipHostMallocDefault);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->done, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->null_ev, hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreate(&c->ev0);
   if (e == hipSuccess) e = hipEventCreate(&c->ev1);
   if (e != hipSuccess) {
@@ -2510,12 +1548,6 @@ int mrag_knn_create(int32_t dim, int32_t device, mrag_knn_index** out) {
   ix->device = device;
   ix->D = dim;
   ix->DP = (dim + 127) / 128 * 128;
-  if (const char* ab = getenv("MRAG_SCAN_ABLATE")) ix->ablate = atoi(ab);
-  if (const char* v1 = getenv("MRAG_SCAN_V1")) ix->scan_v1 = atoi(v1) != 0;
-  if (const char* ns = getenv("MRAG_SCAN_NO_SAMPLE")) ix->no_sample = atoi(ns) != 0;
-  if (const char* v2 = getenv("MRAG_SCAN_V2")) ix->scan_v2 = atoi(v2) != 0;
-  if (const char* v4 = getenv("MRAG_SCAN_V4")) ix->scan_v4 = atoi(v4) != 0;
-  if (const char* v5 = getenv("MRAG_SCAN_V5")) ix->scan_v5 = atoi(v5) != 0;
   hipError_t e = hipStreamCreateWithFlags(&ix->stream, hipStreamNonBlocking);
   if (e != hipSuccess) {
     delete ix;
@@ -2587,6 +1619,7 @@ int mrag_knn_add(mrag_knn_index* ix, const float* rows, const int32_t* labels, i
   hipStream_t s = ix->stream;
   const float* src = rows;
   const int32_t* lsrc = labels;
+  if (ptr_kind == MRAG_PTR_DEVICE) MRAG_HIP(hipStreamSynchronize(nullptr));  // inputs queued on the null stream
   if (ptr_kind == MRAG_PTR_HOST) {
     if (int rc = ensure(ix->stage_rows, (size_t)nrows * ix->D * 4)) return rc;
     if (int rc = ensure(ix->stage_labels, (size_t)nrows * 4)) return rc;
@@ -2649,6 +1682,11 @@ int mrag_knn_search(mrag_knn_index* ix, const float* queries, int64_t nq, int32_
   MRAG_REQUIRE(queries && out_scores && out_rows, "NULL query/output pointer");
   hipStream_t s = stream_arg ? (hipStream_t)stream_arg : ix->stream;
   const bool host = ptr_kind == MRAG_PTR_HOST;
+  if (!host && !stream_arg)
+    if (int rc = mrag::wait_null_stream(c->null_ev, s)) return rc;
+  // destroyed before the lease and the shared lock: an error after the first launch drains s
+  // before the context returns to the pool and mutations may free the corpus buffers
+  mrag::StreamDrain drain(s);
   const int D = ix->D, DP = ix->DP;
   const int64_t nout = nq * k;
 
@@ -2709,20 +1747,20 @@ int mrag_knn_search(mrag_knn_index* ix, const float* queries, int64_t nq, int32_
       return rc;
     if (int rc = mrag_knn::search_generic(generic_args(), c->gws, s, nullptr)) return rc;
   } else {
-    // v2 (64 queries/wave, KL = 8) unless k is deep enough to want longer per-lane lists
-    // (per-lane lists of 8; for 32 < k <= 64 the union of the S split lists still holds
-    // S * 8 >= k + 32 candidates at the batch sizes that matter, and the certificate
-    // sends any query whose top-k a list could not hold to the collect pass)
-    const bool use_v2 = k <= 64 && !ix->scan_v1 && (ix->ablate == 0 || ix->ablate >= 10);
-    // v3 (MFMA 16x16x32, same lists / outputs) unless v2 is forced or a v2 ablation is asked for
-    const bool use_v3 = use_v2 && !ix->scan_v2 && (ix->ablate == 0 || ix->ablate >= 20);
-    // query slots: v2 reads every slot of its query group (no lane guard), so pad to a
-    // whole group; padding rows are zero (prep) and never reach the output
-    const int64_t qpad = use_v2 ? QPG : QPW;
+    // v3 (MFMA 16x16x32, 64 queries per wave, per-lane lists of 6 folded to 8 per split) unless
+    // k is deep enough to want longer per-lane lists (v1). For 32 < k <= 64 the union of the S
+    // split lists still holds S * 8 >= k + 32 candidates at the batch sizes that matter, and the
+    // certificate sends any query whose top-k a list could not hold to the collect pass.
+    const bool use_v3 = k <= 64;
+    const int qb = use_v3 ? scan3_qb(nq) : 4;
+    const int qpg = use_v3 ? 64 * qb : QPG;  // queries per scan workgroup
+    // query slots: v3 reads every slot of its query group (no lane guard), so pad to a whole
+    // group; padding rows are zero (prep) and never reach the output
+    const int64_t qpad = use_v3 ? qpg : QPW;
     const int64_t Qp = (nq + qpad - 1) / qpad * qpad;
-    const int qgroups = (int)((Qp + QPG - 1) / QPG);
+    const int qgroups = (int)((Qp + qpg - 1) / qpg);
     const int ntiles = (int)((ix->n + TILE_ROWS - 1) / TILE_ROWS);
-    const int KL = use_v2 ? 8 : kl_for(k, DP);
+    const int KL = use_v3 ? 8 : kl_for(k, DP);
     int S = std::max(1, 256 / qgroups);
     S = std::min(S, ntiles);
     S = std::min(S, MAX_MERGE_ENTRIES / KL);
@@ -2774,65 +1812,28 @@ int mrag_knn_search(mrag_knn_index* ix, const float* queries, int64_t nq, int32_
     sp.k = k;
     sp.part_tau = use_v3 ? (float*)c->part_tau.p : nullptr;
 
-    const bool use_v4 = use_v3 && ix->scan_v4;
-    const bool use_v5 = use_v3 && !use_v4 && ix->scan_v5;
-    // v5 tiles are 48 rows: its scan and pre-pass walk ntiles5 tiles (the collect pass keeps 64)
-    const int ntiles5 = (int)((ix->n + T5_ROWS - 1) / T5_ROWS);
-    if (use_v5) sp.ntiles = ntiles5;
-    scan_fn scan = use_v5   ? get_scan5(DP)
-                   : use_v4 ? get_scan4(DP)
-                   : use_v3 ? get_scan3(DP)
-                   : use_v2 ? get_scan2(DP)
-                            : get_scan(DP, KL, false);
-    if (DP == 512 && use_v3 && ix->ablate > 20) {  // timing only
-      switch (ix->ablate) {
-        case 21: scan = knn_scan3_kernel<512, 1>; break;
-        case 24: scan = knn_scan3_kernel<512, 4>; break;
-        default: break;
-      }
-    }
-    if (DP == 512 && ix->ablate > 10) {  // timing only
-      switch (ix->ablate) {
-        case 11: scan = knn_scan2_kernel<512, 1>; break;
-        case 12: scan = knn_scan2_kernel<512, 2>; break;
-            case 14: scan = knn_scan2_kernel<512, 4>; break;
-        default: break;
-      }
-    }
-    if (ix->ablate == 1 && DP == 512) scan = knn_scan_kernel<512, 8, false, true>;  // timing only
-    scan_fn collect = get_scan(DP, 8, true);
+    const scan_fn scan = use_v3 ? get_scan3(DP, false, qb) : get_scan(DP, KL, false);
+    const scan_fn collect = get_scan(DP, 8, true);
     if (!scan || !collect) return mrag::fail(MRAG_ERR_UNSUPPORTED, "no scan kernel for DP=%d", DP);
     const dim3 sgrid((unsigned)(qgroups * S));
-    // Sample pre-pass (v2 only, when every split has >= 64 tiles): seeds the shared
-    // threshold near the k-th best so the main scan's list insertions stay rare.
-    static const int sample_stride = [] {  // env MRAG_SAMPLE_STRIDE (A/B timing); default 16
-      const char* e = getenv("MRAG_SAMPLE_STRIDE");
-      const int v = e ? atoi(e) : 16;
-      return v >= 2 ? v : 16;
-    }();
-    const int min_tiles = sp.ntiles / S;
-    if (use_v2 && !ix->no_sample && min_tiles >= 4 * sample_stride) {
-      sp.sample_stride = sample_stride;
-      sp.sample_tiles = min_tiles / sample_stride;
-      if (use_v4)
-        hipLaunchKernelGGL(get_scan4(DP, true), sgrid, dim3(SCAN4_THREADS), 0, s, sp);
-      else if (use_v5)
-        hipLaunchKernelGGL(get_scan5(DP, true), sgrid, dim3(SCAN2_THREADS), 0, s, sp);
-      else
-        hipLaunchKernelGGL(use_v3 ? get_scan3(DP, true) : get_scan2(DP, true), sgrid, dim3(SCAN2_THREADS), 0, s, sp);
+    // Sample pre-pass (v3, when every split has >= 4 * SAMPLE_STRIDE tiles): seeds the shared
+    // threshold near the k-th best so the main scan's list insertions stay rare. Four maxima per
+    // (split, query), one per lane group (merging them in pairs, the round-1 seed, measured 0.2 %
+    // slower in the main scan); stride 16 (32: +5 %, 64: +14 %, none: +70 % scan time).
+    const int min_tiles = ntiles / S;
+    if (use_v3 && min_tiles >= 4 * SAMPLE_STRIDE) {
+      sp.sample_stride = SAMPLE_STRIDE;
+      sp.sample_tiles = min_tiles / SAMPLE_STRIDE;
+      hipLaunchKernelGGL(get_scan3(DP, true, qb), sgrid, dim3(SCAN2_THREADS), 0, s, sp);
       MRAG_CHECK_LAUNCH();
-      // sample maxima per (split, query): 4 from the v3 pre-pass (one per lane group; merging them
-      // in pairs, the round-1 seed, measured 0.2 % slower in the main scan), 2 from the others
-      const int per = (use_v3 && !use_v4 && !use_v5) ? 4 : 2;
-      hipLaunchKernelGGL(theta_init_kernel, dim3((unsigned)nq), dim3(64), 0, s, (const float*)sp.part_s, per * S,
-                         (int)Qp, k, sp.theta, per);
+      hipLaunchKernelGGL(theta_init_kernel, dim3((unsigned)nq), dim3(64), 0, s, (const float*)sp.part_s, 4 * S,
+                         (int)Qp, k, sp.theta);
       MRAG_CHECK_LAUNCH();
     }
     if (profile) MRAG_HIP(hipEventRecord(c->ev0, s));
-    hipLaunchKernelGGL(scan, sgrid, dim3(use_v4 ? SCAN4_THREADS : use_v2 ? SCAN2_THREADS : SCAN_THREADS), 0, s, sp);
+    hipLaunchKernelGGL(scan, sgrid, dim3(use_v3 ? SCAN2_THREADS : SCAN_THREADS), 0, s, sp);
     MRAG_CHECK_LAUNCH();
     if (profile) MRAG_HIP(hipEventRecord(c->ev1, s));
-    sp.ntiles = ntiles;  // 64-row tiles for the collect pass
 
     MergeParams mp{};
     mp.part_s = sp.part_s;
@@ -2861,13 +1862,9 @@ int mrag_knn_search(mrag_knn_index* ix, const float* queries, int64_t nq, int32_
     mp.theta = (const uint32_t*)c->theta.p;
     mp.part_tau = sp.part_tau;
     // K8 key selection: the best M + 1 keys (the M candidates and the first one left out) by
-    // the register top-64P fold when they fit, else the full bitonic sort (env MRAG_K8_SORT=1
-    // forces the sort: A/B timing)
-    static const bool k8_sort = [] {
-      const char* e = getenv("MRAG_K8_SORT");
-      return e && atoi(e) == 1;
-    }();
-    const int sel = k8_sort ? 0 : (M + 1 <= 64 ? 1 : (M + 1 <= 128 ? 2 : 0));
+    // the register top-64P fold when they fit, else the full bitonic sort (40.6 -> 36.5 us per
+    // 1000-query search for the fold)
+    const int sel = M + 1 <= 64 ? 1 : (M + 1 <= 128 ? 2 : 0);
     mp.R = sel ? std::max(R, 4 * 64 * sel) : R;  // the fold parks four waves' top-64P in keys[]
     const size_t msh = (size_t)mp.R * 8 + (size_t)Mp * 12 + (size_t)DP * 4 + 64;
     auto merge = sel == 1 ? knn_merge_kernel<1> : sel == 2 ? knn_merge_kernel<2> : knn_merge_kernel<0>;
@@ -2930,6 +1927,7 @@ int mrag_knn_search(mrag_knn_index* ix, const float* queries, int64_t nq, int32_
     if (out_scores64) MRAG_HIP(hipMemcpyAsync(out_scores64, os64, nout * 8, hipMemcpyDeviceToHost, s));
   }
   if (int rc = wait_stream(c, s)) return rc;
+  drain.armed = false;
   std::lock_guard<std::mutex> lk(ix->pool_mu);
   ix->last_uncertified = uncertified;
   ix->last_retries = retries;

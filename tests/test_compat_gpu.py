@@ -262,3 +262,115 @@ def test_clip_model_concurrent_requests(cuda):
     for i in range(len(batches)):
         assert torch.equal(outs[i], serial[i]), i
     assert 1 <= len(m._vision_pool._all) <= 3
+
+
+def test_text_towers_concurrent_requests(cuda):
+    """The drop-in text towers (MiniLM via embed_text_batch's model, CLIP text via
+    get_text_features) serve concurrent callers on handle pools like the image tower: four
+    threads' results equal the serial calls bit for bit (app/ml/embeddings.py:52-70, 94-105)."""
+    import threading
+
+    import torch
+
+    from app.encoders.models import ClipModel, ClipProcessor, MiniLMSentenceModel
+    from app.settings import settings
+
+    mini = MiniLMSentenceModel(settings.models.text)
+    clip = ClipModel(settings.models.clip)
+    proc = ClipProcessor(settings.models.clip)
+    rng = np.random.default_rng(7)
+    words = [f"w{i}" for i in range(500)]
+    groups = [[" ".join(rng.choice(words, int(rng.integers(3, 40)))) for _ in range(20 + 9 * i)] for i in range(8)]
+    s_text = [mini.encode(g) for g in groups]
+    s_clip = [clip.get_text_features(**proc(text=g[:30])).cpu() for g in groups]
+    o_text, o_clip, errs = [None] * 8, [None] * 8, []
+
+    def work(i):
+        try:
+            o_text[i] = mini.encode(groups[i])
+            o_clip[i] = clip.get_text_features(**proc(text=groups[i][:30])).cpu()
+        except Exception as e:  # surfaced below
+            errs.append(e)
+
+    th = [threading.Thread(target=work, args=(i,)) for i in range(8)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+    assert not errs, errs
+    for i in range(8):
+        assert np.array_equal(o_text[i], s_text[i]), i
+        assert torch.equal(o_clip[i], s_clip[i]), i
+    assert 1 <= len(mini._pool._all) <= 3 and 1 <= len(clip._text_pool._all) <= 3
+
+
+def test_workspace_grows_with_batch_alone(cuda):
+    """per-sequence buffers (pooled rows, [CLS] pooler output) grow when the
+    batch grows while batch x length does not (tokenisers pad to the longest sequence). A long
+    B = 1 call followed by a wider batch of short sequences equals the same call on a fresh
+    handle: cross-encoder (B=1, T=300 then B=32, T=9) and CLIP text (B=1, T=60 then B=8, T=7)."""
+    from app.encoders import CLIP_TEXT_B32, GpuEncoder
+    from app.encoders.weights import MSMARCO_MINILM_L6_CE
+
+    rng = np.random.default_rng(11)
+    ce_used, ce_fresh = GpuEncoder(MSMARCO_MINILM_L6_CE), GpuEncoder(MSMARCO_MINILM_L6_CE)
+    ids1 = rng.integers(1000, 2000, (1, 300)).astype(np.int32)
+    ce_used.score_pairs(ids1, np.zeros_like(ids1), np.ones_like(ids1))
+    ids2 = rng.integers(1000, 2000, (32, 9)).astype(np.int32)
+    types2 = np.zeros_like(ids2)
+    types2[:, 5:] = 1
+    a = ce_used.score_pairs(ids2, types2, np.ones_like(ids2))
+    b = ce_fresh.score_pairs(ids2, types2, np.ones_like(ids2))
+    assert np.array_equal(a, b)
+
+    t_used, t_fresh = GpuEncoder(CLIP_TEXT_B32), GpuEncoder(CLIP_TEXT_B32)
+    long_ids = rng.integers(1, 49000, (1, 60)).astype(np.int32)
+    long_ids[0, -1] = 49407
+    t_used.embed_tokens(long_ids, np.ones_like(long_ids))
+    ids = rng.integers(1, 49000, (8, 7)).astype(np.int32)
+    ids[:, -1] = 49407
+    a = t_used.embed_tokens(ids, np.ones_like(ids))
+    b = t_fresh.embed_tokens(ids, np.ones_like(ids))
+    assert np.array_equal(a, b)
+
+
+def test_null_stream_device_inputs_ordered(cuda):
+    """device inputs written by torch kernels on the default (NULL) stream
+    right before the call are read only after those kernels finish — the search and the encoder
+    run on their own streams, which now wait for the NULL stream."""
+    import torch
+
+    from app.encoders import MINILM_L6, GpuEncoder
+    from app.vector_store import FlatIndex
+    from oracle.knn import flat_cosine_topk
+
+    assert torch.cuda.current_stream().cuda_stream == 0
+    rng = np.random.default_rng(12)
+    x = rng.standard_normal((20_000, 384)).astype(np.float32)
+    qh = rng.standard_normal((64, 384)).astype(np.float32)
+    ix = FlatIndex(384)
+    ix.add(x)
+    ref_s, ref_r = flat_cosine_topk(x, np.zeros(len(x), np.int32), qh, 10)
+    big = torch.randn(4096, 4096, device=cuda)
+    for _ in range(3):
+        q = torch.full((64, 384), float("nan"), device=cuda)
+        torch.cuda.synchronize()
+        acc = big
+        for _ in range(8):  # a few ms of default-stream work ahead of the write of q
+            acc = acc @ big * 1e-3
+        q.copy_(torch.from_numpy(qh).to(cuda) + 0 * acc[:64, :384])
+        s, r = ix.search(q, 10)
+        assert np.array_equal(r.cpu().numpy(), ref_r)
+    enc = GpuEncoder(MINILM_L6)
+    ids_h = rng.integers(1000, 2000, (16, 24)).astype(np.int32)
+    ref = enc.embed_tokens(ids_h, np.ones_like(ids_h))
+    for _ in range(3):
+        ids = torch.zeros((16, 24), dtype=torch.int32, device=cuda)
+        mask = torch.ones((16, 24), dtype=torch.int32, device=cuda)
+        torch.cuda.synchronize()
+        acc = big
+        for _ in range(8):
+            acc = acc @ big * 1e-3
+        ids.copy_(torch.from_numpy(ids_h).to(cuda) + (0 * acc[:16, :24]).to(torch.int32))
+        out = enc.embed_tokens(ids, mask)
+        assert np.array_equal(out.cpu().numpy(), ref)

@@ -231,43 +231,6 @@ def test_small_tables_k_above_list_depth(cuda, dim):
             ix.close()
 
 
-@pytest.mark.parametrize("env", [{"MRAG_SCAN_V2": "1"}, {"MRAG_SCAN_FRONT": "1"}, {"MRAG_SCAN_FRONT": "2"}])
-def test_scan_variants_exact(cuda, env):
-    """The A/B scan variants (v2 on 32x32x16; v3 with the next-tile DMA spread 1 or 2 pieces
-    per k-step) are read from the environment once per process: each runs in a child process
-    on a seeded 270k x 512 corpus (pre-pass active) and must match the oracle exactly."""
-    import os
-    import subprocess
-    import sys
-
-    code = r'''
-import sys, numpy as np
-sys.path[:0] = [sys.argv[1], sys.argv[2], sys.argv[3]]
-from _data import clustered_corpus, labels_for
-from app.vector_store import FlatIndex
-from oracle.knn import flat_cosine_topk
-x = clustered_corpus(270_000, 512, 21, n_clusters=64, spread=0.05, dup_frac=0.05)
-lab = labels_for(len(x), 3, 22)
-rng = np.random.default_rng(23)
-q = np.concatenate([x[rng.integers(0, len(x), 300)] + 0.01 * rng.standard_normal((300, 512)).astype(np.float32),
-                    rng.standard_normal((300, 512)).astype(np.float32)])
-ix = FlatIndex(512)
-ix.add(x, lab)
-for k, f in ((10, -1), (12, 1), (50, -1)):
-    s, r = ix.search(q, k, label=f)
-    os_, or_ = flat_cosine_topk(x, lab, q, k, label_filter=f)
-    assert np.array_equal(r, or_), (k, f)
-    v = or_ >= 0
-    assert np.allclose(s[v], os_[v].astype(np.float32), rtol=0, atol=1e-6), (k, f)
-print("ok")
-'''
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    res = subprocess.run([sys.executable, "-c", code, os.path.join(root, "multimodal-rag-for-image-text-search_amd"),
-                          root, os.path.join(root, "tests")], env=dict(os.environ, **env), capture_output=True,
-                         text=True, timeout=280)
-    assert res.returncode == 0 and "ok" in res.stdout, res.stderr[-2000:]
-
-
 def test_lane_list_overflow_bound(cuda):
     """Adversarial layout for K7 v3's per-lane lists: 45 near-duplicates of query 0 planted on
     the rows one lane group of one split sees (tiles 0, 256, 512 of a 256-split scan, rows
@@ -358,3 +321,32 @@ def test_concurrent_searches_own_streams(cuda):
     ix.add(extra)
     s, r = ix.search(torch.from_numpy(extra).to(cuda), 1)
     assert (r.cpu().numpy()[:, 0] == np.arange(30000, 30010)).all()
+
+
+@pytest.mark.parametrize("dim,k", [(512, 10), (384, 50)])
+def test_small_batches_k7s_prepass(cuda, dim, k):
+    """K7s (the 64-query scan instance that small batches take: the reference issues ONE query
+    per search, app/ml/retrieve.py:53,84) on 2^20 rows, so every one of its 256 splits holds 64
+    tiles and the sample pre-pass seeds the threshold: clustered near-duplicates + exact
+    duplicates, batches of 1, 7 and 64 queries, with and without a label prefilter, against the
+    exact oracle (bit-exact rows, f32 scores)."""
+    from app.vector_store import FlatIndex
+
+    x = clustered_corpus(1 << 20, dim, 31, n_clusters=256, spread=0.05, dup_frac=0.02)
+    lab = labels_for(len(x), 3, 32)
+    rng = np.random.default_rng(33)
+    q = np.concatenate([x[rng.integers(0, len(x), 40)] + 0.01 * rng.standard_normal((40, dim)).astype(np.float32),
+                        rng.standard_normal((24, dim)).astype(np.float32)])
+    ix = FlatIndex(dim)
+    ix.add(x, lab)
+    for nq in (1, 7, 64):
+        for f in (-1, 1):
+            s, r = ix.search(q[:nq], k, label=f)
+            os_, or_ = flat_cosine_topk(x, lab, q[:nq], k, label_filter=f)
+            _check(s, r, os_, or_)
+    # one query at a time equals the batch (the reference's call pattern vs a batch)
+    sb, rb = ix.search(q[:16], k)
+    for i in range(16):
+        s1, r1 = ix.search(q[i], k)
+        np.testing.assert_array_equal(r1[0], rb[i])
+        np.testing.assert_array_equal(s1[0], sb[i])
