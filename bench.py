@@ -670,7 +670,7 @@ def main():
 
     call_pattern = None
     if world == 1 and not args.no_call_pattern:
-        call_pattern = call_pattern_leg(index, q)
+        call_pattern = call_pattern_leg(index, q, reps=max(50, 10 * args.steps))
 
     fusion = None
     if not args.no_fusion:  # config 5 (all ranks take part: sharded corpora + all-gathers)
