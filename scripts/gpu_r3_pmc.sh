@@ -17,3 +17,7 @@ for P in "$P1" "$P2" "$P3" "$P4"; do
 done
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/r3pmc_stats -o run -- $CMD > $R/gpurun_out/r3pmc_stats.log 2>&1 || exit 20
 cd $R && python3 scripts/pmc_kernels.py gpurun_out/r3_pmc_kernels.json gpurun_out/r3pmc_p1 gpurun_out/r3pmc_p2 gpurun_out/r3pmc_p3 gpurun_out/r3pmc_p4 || exit 21
+# keep the reduced counters and the stats summary; the per-dispatch CSVs exceed what gpurun copies back
+cp gpurun_out/r3pmc_stats/*kernel_stats.csv gpurun_out/r3_pmc_kernel_stats.csv 2>/dev/null
+rm -rf gpurun_out/r3pmc_p1 gpurun_out/r3pmc_p2 gpurun_out/r3pmc_p3 gpurun_out/r3pmc_p4 gpurun_out/r3pmc_stats
+ls -la gpurun_out; du -sh gpurun_out

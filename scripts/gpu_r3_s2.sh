@@ -9,4 +9,5 @@ for round in 1 2; do
   done
   MRAG_K7S_NOSAMPLE=1 timeout -k 10 120 python scripts/knn_scan_ab.py 30 >> gpurun_out/r3s2_k7v.log 2>&1 || exit 2
 done
+cat gpurun_out/r3s2_k7v.log
 bash scripts/gpu_r3_pmc.sh || exit 3
