@@ -308,6 +308,13 @@ __device__ __forceinline__ void vmcnt_wait(int n) {  // n wave-uniform, 0..63
   }
 }
 #undef MRAG_VMCNT_CASE
+// compile-time count: one s_waitcnt, never merged with the dynamic ladder above (which the
+// compiler lowers to a compare/branch tree of ~20 scalar instructions per call)
+template <int N>
+__device__ __forceinline__ void vmcnt_wait_c() {
+  static_assert(N >= 0 && N < 64, "vmcnt field is 6 bits");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
 
 template <int EPI>
 __global__ __launch_bounds__(G8_THREADS) void gemm_8p_kernel(GemmArgs g) {
@@ -456,6 +463,7 @@ __global__ __launch_bounds__(G8_THREADS) void gemm_8p_kernel(GemmArgs g) {
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
   };
+  constexpr int ST_FULL = ((EPI == EPI_F32_RESIDUAL || EPI == EPI_F32) ? 2 : 1) * 2 * 2 * NI;
   int st_phi = -100;  // last phase before the most recent epilogue
   int st_cnt = 0;     // vector stores that epilogue issued (wave-uniform)
   // end of a read segment: issue L[phi + 7] (slot SL), wait for L[phi + 2] (read by phase
@@ -474,7 +482,9 @@ __global__ __launch_bounds__(G8_THREADS) void gemm_8p_kernel(GemmArgs g) {
     if (full) stage_slot(SL);
     const bool post = phi - st_phi <= 5;  // the last epilogue's stores are younger than L[phi + 2]
     if (__builtin_expect(full && !post, 1)) {
-      vmcnt_wait(YSTEADY);
+      vmcnt_wait_c<YSTEADY>();
+    } else if (full && st_cnt == ST_FULL) {  // after a tile with every row valid
+      vmcnt_wait_c<YSTEADY + ST_FULL>();
     } else if (full) {
       vmcnt_wait(YSTEADY + st_cnt);
     } else {
@@ -558,224 +568,6 @@ __global__ __launch_bounds__(G8_THREADS) void gemm_8p_kernel(GemmArgs g) {
     }
   }
   if (wr == 0) bar();  // same barrier count for both groups
-}
-
-// ---------------------------------------------------------------------------
-// K3f (M >= 1024): persistent, one workgroup of FOUR waves per CU (2 x 2, one per SIMD), a 256 x BN
-// tile per round (waves of 128 x BN/2; BN = 256, or 192 where N % 256 != 0 or 256-wide tiles
-// would leave CUs idle), 64-deep K-tiles double-buffered in LDS, operands staged through VGPRs:
-// every thread's buffer_load_dwordx4 of K-tile t + 3 is issued in K-tile t's first phase, so a
-// load has two K-tiles of MFMAs to land before its ds_write_b128 (K-tile t + 1's, issued in the
-// same phase) — the prefetch depth the LDS-DMA kernels (K3d, K3e) cannot reach in 128 KiB of LDS.
-//  * per K-tile a wave issues 128 MFMA 16x16x32 (its 8 x NJ blocks over two 32-deep halves); the
-//    fragments of the next half are read from LDS right after the MFMAs that last used their
-//    registers (A ring of 8, W fragments double-buffered); one barrier per K-tile, between the
-//    halves: before it every wave's ds_writes of K-tile t + 1 and its reads of K-tile t are done,
-//    after it the second half reads only K-tile t + 1 (its first-half fragments);
-//  * rows past M read as zero (buffer range check) and are never stored; chunk c of LDS row j sits
-//    at c ^ ((j >> 1) & 7) (conflict-free ds_read_b128, as K3 / K3d);
-//  * weight rows are permuted in LDS (g8-style) so a lane's two 16 x 16 blocks of a pair hold 8
-//    consecutive output columns: gemm_store8, the same per-element accumulation order (32-deep
-//    chunks, ascending k, one accumulator) and epilogue as K3 / K3d: bit-identical results;
-//  * tiles: XCD x owns a contiguous range of tile ids (tm-major), dealt round-robin to its
-//    workgroups, so a 256-row activation panel stays in that XCD's L2.
-constexpr int GF_THREADS = 256;
-
-// acc += W-fragment . A-fragment with the accumulator in AGPRs (a wave's 8 x NJ blocks need all 256)
-__device__ __forceinline__ void mfma_acc(f32x4& acc, const half8& wf, const half8& af) {
-  asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+a"(acc) : "v"(wf), "v"(af));
-}
-// the same with a zero accumulator in (the first 32-deep chunk of a tile): acc is only ever
-// written by MFMAs, so the compiler keeps it in AGPRs
-__device__ __forceinline__ void mfma_acc0(f32x4& acc, const half8& wf, const half8& af) {
-  asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, 0" : "=&a"(acc) : "v"(wf), "v"(af));
-}
-
-template <int EPI, int BN>
-__global__ __launch_bounds__(GF_THREADS, 1) void gemm_rs_kernel(GemmArgs g) {
-  constexpr int BM = 256;
-  constexpr int WN = BN / 2, NJ = WN / 16, NI = 8;
-  constexpr int A_BYTES = BM * 128, W_BYTES = BN * 128, BUF = A_BYTES + W_BYTES;
-  constexpr int LA = BM * 8 / GF_THREADS, LW = BN * 8 / GF_THREADS, LT = LA + LW;
-  static_assert(NJ % 2 == 0 && NJ <= NI, "pairs of weight blocks, at most one W fragment read per A block");
-  __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = w >> 1, wc = w & 1;
-  const int fr = lane & 15, fq = lane >> 4;
-
-  const int tiles_n = g.N / BN;
-  const int ntiles = ((g.M + BM - 1) / BM) * tiles_n;
-  const int xcd = blockIdx.x & 7, sidx = blockIdx.x >> 3;
-  const int nbx = ((int)gridDim.x - xcd + 7) >> 3;
-  const int q8 = ntiles >> 3, r8 = ntiles & 7;
-  const int lo = xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8;
-  const int cnt = q8 + (xcd < r8 ? 1 : 0);
-  const int my_n = sidx < cnt ? (cnt - sidx + nbx - 1) / nbx : 0;
-  if (my_n == 0) return;  // whole workgroup, before any barrier
-  const int ktiles = g.K / 64;  // even, >= 2 (launcher)
-
-  // staging: thread tid loads chunk (tid & 7) of LDS rows 32 i + (tid >> 3): A row m0 + that row,
-  // W row n0 + 32 i + wperm (the column the permuted LDS row holds). Rows past M are out of the
-  // A buffer's range and load zeros.
-  const int s = tid >> 3, c = tid & 7;
-  const int wperm = 8 * ((s >> 2) & 3) + 4 * (s >> 4) + (s & 3);
-  const __amdgpu_buffer_rsrc_t rA =
-      __builtin_amdgcn_make_buffer_rsrc((void*)g.A, 0, (int)((int64_t)g.M * g.lda * 2), 0x00020000);
-  const __amdgpu_buffer_rsrc_t rW =
-      __builtin_amdgcn_make_buffer_rsrc((void*)g.W, 0, (int)((int64_t)g.N * g.ldw * 2), 0x00020000);
-  const uint32_t lds_st = (uint32_t)(s * 128 + ((c ^ ((s >> 1) & 7)) * 16));
-  int ld_tile = 0, ld_kt = 0;  // the loader's position in this workgroup's K-tile stream
-  uint32_t vA = 0, vW = 0;      // its per-thread byte offsets for the current tile
-  auto ld_tile_origin = [&]() {
-    const int T = lo + sidx + ld_tile * nbx;
-    const int tm = T / tiles_n;
-    vA = (uint32_t)((tm * BM + s) * g.lda * 2 + c * 16);
-    vW = (uint32_t)(((T - tm * tiles_n) * BN + wperm) * g.ldw * 2 + c * 16);
-  };
-  ld_tile_origin();
-  u32x4 R[LT];
-  auto load_ktile = [&](u32x4(&R)[LT]) {  // the loader's current K-tile into R, then advance
-    const int k0b = ld_kt * 128;
-#pragma unroll
-    for (int i = 0; i < LA; ++i)
-      R[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rA, vA, i * 32 * g.lda * 2 + k0b, 0));
-#pragma unroll
-    for (int i = 0; i < LW; ++i)
-      R[LA + i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rW, vW, i * 32 * g.ldw * 2 + k0b, 0));
-    if (++ld_kt == ktiles) {
-      ld_kt = 0;
-      if (++ld_tile < my_n) ld_tile_origin();
-    }
-  };
-  auto write_chunk = [&](const u32x4(&R)[LT], int buf, int i) {
-    const uint32_t base = (uint32_t)buf * BUF + (i < LA ? i * 4096 : A_BYTES + (i - LA) * 4096);
-    *(u32x4*)(smem + base + lds_st) = R[i];
-  };
-
-  // fragment offsets: A block i = LDS row 128 wr + 16 i + fr, W block jb = 128... row wc WN + 16 jb + fr;
-  // 32-deep half kk reads chunk 4 kk + fq at position (4 kk + fq) ^ (fr >> 1)
-  uint32_t oA[2], oW[2];
-#pragma unroll
-  for (int kk = 0; kk < 2; ++kk) {
-    oA[kk] = (uint32_t)((128 * wr + fr) * 128 + (((4 * kk + fq) ^ (fr >> 1)) * 16));
-    oW[kk] = (uint32_t)(A_BYTES + (WN * wc + fr) * 128 + (((4 * kk + fq) ^ (fr >> 1)) * 16));
-  }
-  half8 fa[NI], fb0[NJ], fb1[NJ];
-  auto rdA = [&](int buf, int kk, int i) { return *(const half8*)(smem + buf * BUF + oA[kk] + i * 2048); };
-  auto rdW = [&](int buf, int kk, int jb) { return *(const half8*)(smem + buf * BUF + oW[kk] + jb * 2048); };
-
-  f32x4 acc[NI][NJ];  // AGPRs; the first chunk of every tile starts them from zero (mfma_acc0)
-
-  auto bar = [&]() {
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-  };
-
-  // prologue: K-tile 0 into LDS buffer 0, K-tile 1 in flight; K-tile 0's first-half fragments
-  load_ktile(R);
-#pragma unroll
-  for (int i = 0; i < LT; ++i) write_chunk(R, 0, i);
-  load_ktile(R);
-  bar();
-#pragma unroll
-  for (int i = 0; i < NI; ++i) fa[i] = rdA(0, 0, i);
-#pragma unroll
-  for (int jb = 0; jb < NJ; ++jb) fb0[jb] = rdW(0, 0, jb);
-
-  // One K-tile in LDS buffer X. Rn holds K-tile t + 1 (written to LDS buffer X ^ 1 here) and is
-  // reloaded with K-tile t + 2. Every memory operation is unconditional (loads past the stream's
-  // end re-read the last tile, writes past it go to a buffer nobody reads), so no register is
-  // merged across a branch. FIRST: the tile's first K-tile (accumulators start at zero); LAST:
-  // its last (the next tile's first fragments are read after the epilogue, whose values then
-  // hold the fragment registers).
-  auto ktile = [&](auto x_c, auto first_c, auto last_c, u32x4(&Rn)[LT]) {
-    constexpr int X = decltype(x_c)::value;
-    constexpr bool FIRST = decltype(first_c)::value, LAST = decltype(last_c)::value;
-#pragma unroll
-    for (int i = 0; i < NI; ++i) {
-#pragma unroll
-      for (int jb = 0; jb < NJ; ++jb) {
-        if constexpr (FIRST)
-          mfma_acc0(acc[i][jb], fb0[jb], fa[i]);
-        else
-          mfma_acc(acc[i][jb], fb0[jb], fa[i]);
-        if (jb == 0) fa[i] = rdA(X, 1, i);
-        if (jb == 1 && i < NJ) fb1[i] = rdW(X, 1, i);
-        if (jb == 2 && 2 * i < LT) write_chunk(Rn, X ^ 1, 2 * i);
-        if (jb == 3 && 2 * i + 1 < LT) write_chunk(Rn, X ^ 1, 2 * i + 1);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-    load_ktile(Rn);
-    bar();
-#pragma unroll
-    for (int i = 0; i < NI; ++i) {
-#pragma unroll
-      for (int jb = 0; jb < NJ; ++jb) {
-        mfma_acc(acc[i][jb], fb1[jb], fa[i]);
-        if constexpr (!LAST) {
-          if (jb == NJ - 1) fa[i] = rdA(X ^ 1, 0, i);
-          if (jb == NJ - 2 && i < NJ) fb0[i] = rdW(X ^ 1, 0, i);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-  };
-  using F = std::false_type;
-  using Tr = std::true_type;
-  using X0 = std::integral_constant<int, 0>;
-  using X1 = std::integral_constant<int, 1>;
-  for (int tile_i = 0; tile_i < my_n; ++tile_i) {
-    // ktiles is even, so every tile starts in LDS buffer 0 with its K-tile 1 in R
-    if (ktiles == 2) {
-      ktile(X0{}, Tr{}, F{}, R);
-      ktile(X1{}, F{}, Tr{}, R);
-    } else {
-      ktile(X0{}, Tr{}, F{}, R);
-      ktile(X1{}, F{}, F{}, R);
-      for (int kt = 2; kt < ktiles - 2; kt += 2) {
-        ktile(X0{}, F{}, F{}, R);
-        ktile(X1{}, F{}, F{}, R);
-      }
-      ktile(X0{}, F{}, F{}, R);
-      ktile(X1{}, F{}, Tr{}, R);
-    }
-    // epilogue: the MFMAs are asm, so the hazard recognizer cannot space the accumulator reads
-    // from them: let the last ones retire first
-    asm volatile("s_nop 15\n\ts_nop 3" ::: "memory");
-    const int T = lo + sidx + tile_i * nbx;
-    const int tm = T / tiles_n;
-    const int m0 = tm * BM, n0 = (T - tm * tiles_n) * BN;
-#pragma unroll
-    for (int p = 0; p < NJ / 2; ++p) {
-      const int n = n0 + WN * wc + 32 * p + 8 * fq;
-      float bn[8];
-      if (g.bias) {
-        const f32x4 b0 = *(const f32x4*)(g.bias + n), b1 = *(const f32x4*)(g.bias + n + 4);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          bn[r] = b0[r];
-          bn[4 + r] = b1[r];
-        }
-      } else {
-#pragma unroll
-        for (int r = 0; r < 8; ++r) bn[r] = 0.f;
-      }
-#pragma unroll
-      for (int i = 0; i < NI; ++i) {
-        const int m = m0 + 128 * wr + 16 * i + fr;
-        if (m < g.M) gemm_store8<EPI>(g, m, n, acc[i][2 * p], acc[i][2 * p + 1], bn);
-      }
-    }
-    // the next tile's first fragments (K-tile 0 of it is in LDS buffer 0)
-#pragma unroll
-    for (int i = 0; i < NI; ++i) fa[i] = rdA(0, 0, i);
-#pragma unroll
-    for (int jb = 0; jb < NJ; ++jb) fb0[jb] = rdW(0, 0, jb);
-  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1253,39 +1045,8 @@ struct K3Kern {
   static constexpr auto fn = gemm_nt_kernel<EPI>;
 };
 
-template <int EPI>
-struct K3fKern256 {
-  static constexpr auto fn = gemm_rs_kernel<EPI, 256>;
-};
-template <int EPI>
-struct K3fKern192 {
-  static constexpr auto fn = gemm_rs_kernel<EPI, 192>;
-};
-
-// env MRAG_GEMM_K3F (experiment): 1 = K3f where K3d would run (BN 256, or 192 for N % 256 != 0 /
-// N = 768), 2 = K3f BN 256 only, 3 = BN 192 wherever N % 192 == 0
-int k3f_mode() {
-  static const int v = [] {
-    const char* e = getenv("MRAG_GEMM_K3F");
-    return e ? atoi(e) : 0;
-  }();
-  return v;
-}
-
 int launch_gemm(const GemmArgs& g, int epi, hipStream_t s) {
   if (g.M <= 0) return MRAG_OK;
-  if (k3f_mode() != 0 && g.M >= 1024 && g.K % 128 == 0 && (int64_t)g.M * g.lda * 2 < (1ll << 31) &&
-      (int64_t)g.N * g.ldw * 2 < (1ll << 31) && g.lda % 8 == 0 && g.ldw % 8 == 0 && g.ldc % 4 == 0) {
-    const bool b192 = (k3f_mode() == 1 && g.N % 192 == 0 && (g.N % 256 != 0 || g.N == 768)) ||
-                      (k3f_mode() == 3 && g.N % 192 == 0);
-    if (b192 || g.N % 256 == 0) {
-      const int BN = b192 ? 192 : 256;
-      const int ntiles = ((g.M + 255) / 256) * (g.N / BN);
-      const int nb = std::min((ntiles + 7) / 8 * 8, std::max(8, num_cus() / 8 * 8));
-      return b192 ? launch_epi<K3fKern192>(epi, dim3((unsigned)nb), dim3(GF_THREADS), s, g)
-                  : launch_epi<K3fKern256>(epi, dim3((unsigned)nb), dim3(GF_THREADS), s, g);
-    }
-  }
   MRAG_REQUIRE(g.N % GN == 0 && g.K % GK == 0, "gemm: N=%d must be a multiple of %d and K=%d of %d", g.N, GN, g.K,
                GK);
   MRAG_REQUIRE(g.lda % 8 == 0 && g.ldw % 8 == 0 && g.ldc % 4 == 0, "gemm: lda/ldw must be multiples of 8, ldc of 4");

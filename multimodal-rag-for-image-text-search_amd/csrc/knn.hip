@@ -436,10 +436,11 @@ __device__ __forceinline__ void mfma16_guard(f32x4 (&acc)[4][1]) {
 // retrieve_text / retrieve_images, app/ml/retrieve.py:53,84). With one block a tile costs a
 // quarter of the MFMAs, so the scan streams the corpus at the fill / HBM rate instead of
 // padding a single query to 256 (K7s). Lists, thresholds, part_tau and outputs are the same.
-// V (experiment bits, A/B timing; 0 = default): 1 = group-test hits marked unlikely, 2 = tile
-// labels by a global load into a VGPR one tile ahead (no label LDS-DMA / LDS read), 4 = the
-// MFMA -> VALU guard only where the tile is masked, 8 = next-tile DMA 8 pieces per k-step
-template <int DP, int MODE = 0, int QB = 4, int V = 0>
+//
+// MFMA -> VALU distance: the masking below reads this tile's accumulators right after their
+// MFMAs, so it alone pays the s_nop guard; the group tests read them a tile later, at least the
+// rest of that k-step's MFMAs after the last write (r3 A/B: an unconditional guard cost 1%).
+template <int DP, int MODE = 0, int QB = 4>
 __global__ __launch_bounds__(SCAN2_THREADS) void knn_scan3_kernel(ScanParams p) {
   constexpr int KSTEPS = DP / 32;
   constexpr int ROW_BYTES = DP * 2;
@@ -448,7 +449,7 @@ __global__ __launch_bounds__(SCAN2_THREADS) void knn_scan3_kernel(ScanParams p) 
   constexpr int GLDS_PER_WAVE = TILE_BYTES / 1024 / SCAN2_WAVES;
   static_assert(GLDS_PER_WAVE == KSTEPS, "one LDS-DMA piece per k-step");
   static_assert(CPR % 16 == 0, "swizzle needs rows of a multiple of 16 chunks");
-  constexpr int FRONT = (V & 8) ? 8 : 4;
+  constexpr int FRONT = 4;
   constexpr int NGROUPS = 4 * QB;  // group g: query block g >> 2, row block g & 3
   constexpr int QPW3 = 16 * QB, QPG3 = SCAN2_WAVES * QPW3;  // queries per wave / workgroup
   constexpr int LBL_OFF = 2 * TILE_BYTES;
@@ -541,7 +542,6 @@ __global__ __launch_bounds__(SCAN2_THREADS) void knn_scan3_kernel(ScanParams p) 
   };
 
   int prow = 0;  // first row of the filtered tile + 4 g4
-  int lab_cur = 0;  // V & 2: this tile's label per lane, loaded during the previous tile
   auto epi_group = [&](auto g_c, auto y_c) {
     constexpr int G = decltype(g_c)::value;
     constexpr int Y = decltype(y_c)::value;
@@ -552,9 +552,7 @@ __global__ __launch_bounds__(SCAN2_THREADS) void knn_scan3_kernel(ScanParams p) 
       smax[qb] = fmaxf(smax[qb], gm);
       asm volatile("" : "+v"(smax[qb]));
     } else {
-      bool hit = __any(gm > fmaxf(ls[qb][KL3 - 1], theta_f[qb]));
-      if constexpr ((V & 1) != 0) hit = __builtin_expect(hit, 0);
-      if (hit) {
+      if (__any(gm > fmaxf(ls[qb][KL3 - 1], theta_f[qb]))) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const float sv = av[r];
@@ -584,13 +582,7 @@ __global__ __launch_bounds__(SCAN2_THREADS) void knn_scan3_kernel(ScanParams p) 
       for (int qb = 0; qb < QB; ++qb)
         theta_next[qb] = __hip_atomic_load(theta_q + 16 * qb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    int lab;
-    if constexpr ((V & 2) != 0) {
-      lab = lab_cur;
-      lab_cur = p.labels[(size_t)ntile * TILE_ROWS + lane];  // next tile's, retired by the end-of-tile wait
-    } else {
-      lab = ((const int*)(smem + LBL_OFF + X * TILE_ROWS * 4))[lane];
-    }
+    const int lab = ((const int*)(smem + LBL_OFF + X * TILE_ROWS * 4))[lane];
     const bool lab_ok = (p.label_filter == MRAG_LABEL_ANY) ? (lab >= 0) : (lab == p.label_filter);
     const uint64_t tile_mask = __ballot(lab_ok);
     const char* tb = smem + X * TILE_BYTES;
@@ -609,7 +601,7 @@ __global__ __launch_bounds__(SCAN2_THREADS) void knn_scan3_kernel(ScanParams p) 
     };
 #pragma unroll
     for (int rb = 0; rb < 4; ++rb) read_a(0, rb);
-    if constexpr ((V & 2) == 0) stage_labels(Y, ntile);
+    stage_labels(Y, ntile);
     if constexpr (QB == 1) {
       // K7s (fill-bound): every piece of the next tile at the top of the tile, so the DMA has the
       // whole tile to land; per k-step the four row blocks' MFMAs, each followed by its next
@@ -643,19 +635,6 @@ __global__ __launch_bounds__(SCAN2_THREADS) void knn_scan3_kernel(ScanParams p) 
         // one job per MFMA gap
         if constexpr ((j & 3) == 3) {  // after the last MFMA of block rb: its next fragment
           if constexpr (kk + 1 < KSTEPS) read_a(kk + 1, rb);
-        } else if constexpr (FRONT == 8 && ((j & 3) == 1 || (j & 3) == 2)) {  // a whole piece per gap
-          constexpr int pc = 8 * kk + 2 * (j >> 2) + ((j & 3) == 2 ? 1 : 0);
-          if constexpr (pc < GLDS_PER_WAVE) {
-            if constexpr (CPR == 64) {
-              voff = (lane16 ^ (uint32_t)(pc << 4)) + (uint32_t)(pc * 1024);
-              asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1"
-                           : "+v"(voff)
-                           : "s"(gw), "s"(ldsw + pc * 1024)
-                           : "memory");
-            } else {
-              stage_piece(Y, ntile, pc, lane_t);
-            }
-          }
         } else if constexpr ((j & 3) == 1) {  // piece FRONT kk + (j >> 2): m0 + source offset
           constexpr int pc = FRONT * kk + (j >> 2);
           if constexpr (CPR == 64 && (j >> 2) < FRONT && pc < GLDS_PER_WAVE) {
@@ -677,10 +656,9 @@ __global__ __launch_bounds__(SCAN2_THREADS) void knn_scan3_kernel(ScanParams p) 
         __builtin_amdgcn_sched_barrier(0);
       });
     });
-    if constexpr ((V & 4) == 0) mfma16_guard(acc[X]);
     if constexpr (CPR == 64 && QB == 4) asm volatile("s_mov_b32 m0, %0" ::"s"(m0_keep));
     if (tile_mask != ~0ull) {
-      if constexpr ((V & 4) != 0) mfma16_guard(acc[X]);
+      mfma16_guard(acc[X]);
       const uint64_t lm = tile_mask >> (4 * g4);
 #pragma unroll
       for (int rb = 0; rb < 4; ++rb)
@@ -706,10 +684,7 @@ __global__ __launch_bounds__(SCAN2_THREADS) void knn_scan3_kernel(ScanParams p) 
   if (my_tiles > 0) {
 #pragma unroll
     for (int i = 0; i < GLDS_PER_WAVE; ++i) stage_piece(0, split, i, lane);
-    if constexpr ((V & 2) != 0)
-      lab_cur = p.labels[(size_t)split * TILE_ROWS + lane];
-    else
-      stage_labels(0, split);
+    stage_labels(0, split);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     for (int it = 0; it < my_tiles; it += 2) {
@@ -1387,29 +1362,21 @@ int kl_for(int k, int DP) {
   return 32;
 }
 
-scan_fn get_scan3_v(int v) {  // env MRAG_K7_V (experiment): DP = 512, 256-query groups
-  switch (v) {
-    case 1: return knn_scan3_kernel<512, 0, 4, 1>;
-    case 2: return knn_scan3_kernel<512, 0, 4, 2>;
-    case 4: return knn_scan3_kernel<512, 0, 4, 4>;
-    case 8: return knn_scan3_kernel<512, 0, 4, 8>;
-    case 7: return knn_scan3_kernel<512, 0, 4, 7>;
-    case 15: return knn_scan3_kernel<512, 0, 4, 15>;
-    default: return knn_scan3_kernel<512, 0, 4, 0>;
-  }
-}
-
-template <int QB>
-scan_fn get_scan3q(int DP, bool sample) {
+template <int MODE, int QB>
+scan_fn get_scan3m(int DP) {
   switch (DP) {
-    case 128: return sample ? knn_scan3_kernel<128, 1, QB> : knn_scan3_kernel<128, 0, QB>;
-    case 256: return sample ? knn_scan3_kernel<256, 1, QB> : knn_scan3_kernel<256, 0, QB>;
-    case 384: return sample ? knn_scan3_kernel<384, 1, QB> : knn_scan3_kernel<384, 0, QB>;
-    case 512: return sample ? knn_scan3_kernel<512, 1, QB> : knn_scan3_kernel<512, 0, QB>;
+    case 128: return knn_scan3_kernel<128, MODE, QB>;
+    case 256: return knn_scan3_kernel<256, MODE, QB>;
+    case 384: return knn_scan3_kernel<384, MODE, QB>;
+    case 512: return knn_scan3_kernel<512, MODE, QB>;
     default: return nullptr;
   }
 }
-scan_fn get_scan3(int DP, bool sample, int qb) { return qb == 1 ? get_scan3q<1>(DP, sample) : get_scan3q<4>(DP, sample); }
+// the sample pre-pass (MODE 1) exists for the 256-query groups only (K7s runs without it)
+scan_fn get_scan3(int DP, bool sample, int qb) {
+  if (qb == 1) return sample ? nullptr : get_scan3m<0, 1>(DP);
+  return sample ? get_scan3m<1, 4>(DP) : get_scan3m<0, 4>(DP);
+}
 
 // Query blocks per wave of the v3 scan for a batch: 1 (K7s, 64 queries per workgroup) while the
 // padded batch fits one small group, else 4 (256 per workgroup).
@@ -1853,25 +1820,18 @@ int mrag_knn_search(mrag_knn_index* ix, const float* queries, int64_t nq, int32_
     sp.k = k;
     sp.part_tau = use_v3 ? (float*)c->part_tau.p : nullptr;
 
-    static const int k7v = [] {
-      const char* e = getenv("MRAG_K7_V");
-      return e ? atoi(e) : 0;
-    }();
-    const scan_fn scan = use_v3 ? (DP == 512 && qb == 4 && k7v ? get_scan3_v(k7v) : get_scan3(DP, false, qb))
-                                : get_scan(DP, KL, false);
+    const scan_fn scan = use_v3 ? get_scan3(DP, false, qb) : get_scan(DP, KL, false);
     const scan_fn collect = get_scan(DP, 8, true);
     if (!scan || !collect) return mrag::fail(MRAG_ERR_UNSUPPORTED, "no scan kernel for DP=%d", DP);
     const dim3 sgrid((unsigned)(qgroups * S));
     // Sample pre-pass (v3, when every split has >= 4 * SAMPLE_STRIDE tiles): seeds the shared
     // threshold near the k-th best so the main scan's list insertions stay rare. Four maxima per
     // (split, query), one per lane group (merging them in pairs, the round-1 seed, measured 0.2 %
-    // slower in the main scan); stride 16 (32: +5 %, 64: +14 %, none: +70 % scan time).
+    // slower in the main scan); stride 16 (32: +5 %, 64: +14 %, none: +70 % scan time). K7s
+    // (qb == 1) streams at the HBM rate, where the pre-pass costs more than the inserts it saves
+    // (Q = 1: 0.270 -> 0.247 ms without it, notes/knn_scan_experiments.md).
     const int min_tiles = ntiles / S;
-    static const bool k7s_nosample = [] {  // env MRAG_K7S_NOSAMPLE=1 (experiment): no pre-pass on K7s
-      const char* e = getenv("MRAG_K7S_NOSAMPLE");
-      return e && atoi(e) == 1;
-    }();
-    if (use_v3 && min_tiles >= 4 * SAMPLE_STRIDE && !(qb == 1 && k7s_nosample)) {
+    if (use_v3 && qb == 4 && min_tiles >= 4 * SAMPLE_STRIDE) {
       sp.sample_stride = SAMPLE_STRIDE;
       sp.sample_tiles = min_tiles / SAMPLE_STRIDE;
       hipLaunchKernelGGL(get_scan3(DP, true, qb), sgrid, dim3(SCAN2_THREADS), 0, s, sp);

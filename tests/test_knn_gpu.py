@@ -324,10 +324,10 @@ def test_concurrent_searches_own_streams(cuda):
 
 
 @pytest.mark.parametrize("dim,k", [(512, 10), (384, 50)])
-def test_small_batches_k7s_prepass(cuda, dim, k):
+def test_small_batches_k7s(cuda, dim, k):
     """K7s (the 64-query scan instance that small batches take: the reference issues ONE query
     per search, app/ml/retrieve.py:53,84) on 2^20 rows, so every one of its 256 splits holds 64
-    tiles and the sample pre-pass seeds the threshold: clustered near-duplicates + exact
+    tiles and the threshold starts unseeded (K7s runs without the pre-pass): clustered near-duplicates + exact
     duplicates, batches of 1, 7 and 64 queries, with and without a label prefilter, against the
     exact oracle (bit-exact rows, f32 scores)."""
     from app.vector_store import FlatIndex
