@@ -80,6 +80,18 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
+namespace mrag {
+// compile-time loop: f(std::integral_constant<int, i>) for i = 0 .. N - 1, fully unrolled
+template <typename F, int... I>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+}  // namespace mrag
+
 // Monotone float -> uint32 map (ascending float == ascending uint).
 __device__ __forceinline__ uint32_t mrag_f2ord(float f) {
   uint32_t u = __float_as_uint(f);

@@ -375,14 +375,7 @@ constexpr int SCAN2_THREADS = SCAN2_WAVES * 64;
 constexpr int QPW2 = 64;  // two 32-query blocks per wave
 static_assert(SCAN2_WAVES * QPW2 == QPG, "v3 keeps the query-group size of v1");
 
-template <typename F, int... I>
-__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
-  (f(std::integral_constant<int, I>{}), ...);
-}
-template <int N, typename F>
-__device__ __forceinline__ void static_for(F&& f) {
-  static_for_impl(f, std::make_integer_sequence<int, N>{});
-}
+using mrag::static_for;
 // ---------------------------------------------------------------------------
 // K7 v3 (top-k mode): v2's pipeline on MFMA 16x16x32. At equal cycles per FLOP the chip holds
 // a higher clock on the 16x16x32 shape than on 32x32x16 with operands re-read from LDS
@@ -440,6 +433,16 @@ __device__ __forceinline__ void mfma16_guard(f32x4 (&acc)[4][1]) {
 // MFMA -> VALU distance: the masking below reads this tile's accumulators right after their
 // MFMAs, so it alone pays the s_nop guard; the group tests read them a tile later, at least the
 // rest of that k-step's MFMAs after the last write (r3 A/B: an unconditional guard cost 1%).
+#ifdef MRAG_K7_STAMPS
+// Diagnostic build only (make stamp -> lib/libmrag_k7stamp.so): per wave, summed shader-clock
+// spans of each tile's segments, [wave][K7_NSTAMP]; no other code reads them.
+constexpr int K7_NSTAMP = 8, K7_MAXWAVES = 1 << 16;
+__device__ unsigned long long g_k7_stamps[K7_MAXWAVES * K7_NSTAMP];
+#define K7_STAMP(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#else
+#define K7_STAMP(v)
+#endif
+
 template <int DP, int MODE = 0, int QB = 4>
 __global__ __launch_bounds__(SCAN2_THREADS) void knn_scan3_kernel(ScanParams p) {
   constexpr int KSTEPS = DP / 32;
@@ -490,6 +493,7 @@ __global__ __launch_bounds__(SCAN2_THREADS) void knn_scan3_kernel(ScanParams p) 
   float ls[QB][KL3];
   int li[QB][KL3];
   float theta_f[QB], published[QB];
+  float thr[QB];  // fmaxf(ls[qb][KL3 - 1], theta_f[qb]): the group test's threshold
   uint32_t theta_next[QB];
 #pragma unroll
   for (int qb = 0; qb < QB; ++qb) {
@@ -499,6 +503,7 @@ __global__ __launch_bounds__(SCAN2_THREADS) void knn_scan3_kernel(ScanParams p) 
       li[qb][j] = -1;
     }
     theta_f[qb] = -INFINITY;
+    thr[qb] = -INFINITY;
     published[qb] = -INFINITY;
     theta_next[qb] = 0u;
   }
@@ -542,17 +547,28 @@ __global__ __launch_bounds__(SCAN2_THREADS) void knn_scan3_kernel(ScanParams p) 
   };
 
   int prow = 0;  // first row of the filtered tile + 4 g4
+#ifdef MRAG_K7_STAMPS
+  // [0] tile top -> end of the DMA k-steps, [1] -> last MFMA issued, [2] -> tail + vmcnt(0),
+  // [3] -> after the barrier, [4] tiles
+  unsigned long long st_sum[5] = {0, 0, 0, 0, 0}, st_mid = 0;
+#endif
   auto epi_group = [&](auto g_c, auto y_c) {
     constexpr int G = decltype(g_c)::value;
     constexpr int Y = decltype(y_c)::value;
     constexpr int qb = G >> 2, rb = G & 3;
     f32x4& av = acc[Y][rb][qb];
-    const float gm = fmaxf(fmaxf(av[0], av[1]), fmaxf(av[2], av[3]));
+    // two VALU ops for the group maximum: the accumulators come out of inline asm, so fmaxf
+    // would first canonicalise each operand (v_max x, x); scores are never NaN
+    float gm;
+    asm("v_max3_f32 %0, %1, %2, %3\n\tv_max_f32 %0, %0, %4"
+        : "=&v"(gm)
+        : "v"(av[0]), "v"(av[1]), "v"(av[2]), "v"(av[3]));
     if constexpr (MODE == 1) {
-      smax[qb] = fmaxf(smax[qb], gm);
-      asm volatile("" : "+v"(smax[qb]));
+      float sm = smax[qb];
+      asm volatile("v_max_f32 %0, %0, %1" : "+v"(sm) : "v"(gm));
+      smax[qb] = sm;
     } else {
-      if (__any(gm > fmaxf(ls[qb][KL3 - 1], theta_f[qb]))) {
+      if (__any(gm > thr[qb])) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const float sv = av[r];
@@ -564,6 +580,7 @@ __global__ __launch_bounds__(SCAN2_THREADS) void knn_scan3_kernel(ScanParams p) 
           __hip_atomic_fetch_max(theta_q + 16 * qb, mrag_f2ord(published[qb]), __ATOMIC_RELAXED,
                                  __HIP_MEMORY_SCOPE_AGENT);
         }
+        thr[qb] = fmaxf(ls[qb][KL3 - 1], theta_f[qb]);
       }
     }
   };
@@ -571,6 +588,7 @@ __global__ __launch_bounds__(SCAN2_THREADS) void knn_scan3_kernel(ScanParams p) 
   auto tile_body = [&](auto x_c, int it) {
     constexpr int X = decltype(x_c)::value;
     constexpr int Y = 1 - X;
+    K7_STAMP(st0);
     const int tile = split + it * tstep;
     const bool has_next = it + 1 < my_tiles;
     const int ntile = has_next ? tile + tstep : tile;
@@ -582,9 +600,6 @@ __global__ __launch_bounds__(SCAN2_THREADS) void knn_scan3_kernel(ScanParams p) 
       for (int qb = 0; qb < QB; ++qb)
         theta_next[qb] = __hip_atomic_load(theta_q + 16 * qb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    const int lab = ((const int*)(smem + LBL_OFF + X * TILE_ROWS * 4))[lane];
-    const bool lab_ok = (p.label_filter == MRAG_LABEL_ANY) ? (lab >= 0) : (lab == p.label_filter);
-    const uint64_t tile_mask = __ballot(lab_ok);
     const char* tb = smem + X * TILE_BYTES;
     int lane_t = lane, offA0 = offA0_init;
     uint32_t lane16 = lane * 16;
@@ -595,12 +610,17 @@ __global__ __launch_bounds__(SCAN2_THREADS) void knn_scan3_kernel(ScanParams p) 
     uint32_t m0_keep = 0;
     uint32_t voff = 0;
     if constexpr (CPR == 64 && QB == 4) asm volatile("s_mov_b32 %0, m0" : "=s"(m0_keep));
-    half8 a[4];
+    // A fragments: fragment n = 4 kk + rb sits in a[n % NA]. QB = 4 keeps five, so fragment
+    // n + 5 is read as soon as fragment n's MFMAs are issued: 16 MFMAs before its first use
+    // (four buffers would give 12, which LDS latency under the DMA writes can exceed)
+    constexpr int NA = QB == 4 ? 5 : 4;
+    half8 a[NA];
     auto read_a = [&](int kk, int rb) {
-      a[rb] = *(const half8*)(tb + ((offA0 ^ ((kk & 3) << 6)) + (kk >> 2) * 256 + rb * 16 * ROW_BYTES));
+      a[(4 * kk + rb) % NA] =
+          *(const half8*)(tb + ((offA0 ^ ((kk & 3) << 6)) + (kk >> 2) * 256 + rb * 16 * ROW_BYTES));
     };
 #pragma unroll
-    for (int rb = 0; rb < 4; ++rb) read_a(0, rb);
+    for (int n = 0; n < NA; ++n) read_a(n >> 2, n & 3);
     stage_labels(Y, ntile);
     if constexpr (QB == 1) {
       // K7s (fill-bound): every piece of the next tile at the top of the tile, so the DMA has the
@@ -613,9 +633,9 @@ __global__ __launch_bounds__(SCAN2_THREADS) void knn_scan3_kernel(ScanParams p) 
         static_for<4>([&](auto rb_c) {
           constexpr int rb = decltype(rb_c)::value;
           if constexpr (kk == 0)
-            mfma16_ab0(acc[X][rb][0], a[rb], qf[kk][0]);
+            mfma16_ab0(acc[X][rb][0], a[(4 * kk + rb) % NA], qf[kk][0]);
           else
-            mfma16_ab(acc[X][rb][0], a[rb], qf[kk][0]);
+            mfma16_ab(acc[X][rb][0], a[(4 * kk + rb) % NA], qf[kk][0]);
           if constexpr (kk + 1 < KSTEPS) read_a(kk + 1, rb);
           if constexpr (kk == 0) epi_group(std::integral_constant<int, rb>{}, std::integral_constant<int, Y>{});
           __builtin_amdgcn_sched_barrier(0);
@@ -628,13 +648,14 @@ __global__ __launch_bounds__(SCAN2_THREADS) void knn_scan3_kernel(ScanParams p) 
       static_for<16>([&](auto j_c) {
         constexpr int j = decltype(j_c)::value;
         constexpr int rb = j >> 2, qb = j & 3;
+        constexpr int n = 4 * kk + rb;  // this MFMA's A fragment
         if constexpr (kk == 0)
-          mfma16_ab0(acc[X][rb][qb], a[rb], qf[kk][qb]);
+          mfma16_ab0(acc[X][rb][qb], a[n % NA], qf[kk][qb]);
         else
-          mfma16_ab(acc[X][rb][qb], a[rb], qf[kk][qb]);
+          mfma16_ab(acc[X][rb][qb], a[n % NA], qf[kk][qb]);
         // one job per MFMA gap
-        if constexpr ((j & 3) == 3) {  // after the last MFMA of block rb: its next fragment
-          if constexpr (kk + 1 < KSTEPS) read_a(kk + 1, rb);
+        if constexpr ((j & 3) == 3) {  // after the last MFMA of fragment n: fragment n + NA
+          if constexpr (n + NA < 4 * KSTEPS) read_a((n + NA) >> 2, (n + NA) & 3);
         } else if constexpr ((j & 3) == 1) {  // piece FRONT kk + (j >> 2): m0 + source offset
           constexpr int pc = FRONT * kk + (j >> 2);
           if constexpr (CPR == 64 && (j >> 2) < FRONT && pc < GLDS_PER_WAVE) {
@@ -653,10 +674,19 @@ __global__ __launch_bounds__(SCAN2_THREADS) void knn_scan3_kernel(ScanParams p) 
           if constexpr (g0 + (j >> 2) < g1)
             epi_group(std::integral_constant<int, g0 + (j >> 2)>{}, std::integral_constant<int, Y>{});
         }
+#ifdef MRAG_K7_STAMPS
+        if constexpr (kk == (GLDS_PER_WAVE + FRONT - 1) / FRONT - 1 && j == 15) st_mid = __builtin_amdgcn_s_memtime();
+#endif
         __builtin_amdgcn_sched_barrier(0);
       });
     });
+    K7_STAMP(st1);
     if constexpr (CPR == 64 && QB == 4) asm volatile("s_mov_b32 m0, %0" ::"s"(m0_keep));
+    // the tile's labels, read after its MFMAs (a read at the top would wait for its LDS
+    // round trip before the first MFMA; buffer X is not rewritten before the barrier)
+    const int lab = ((const int*)(smem + LBL_OFF + X * TILE_ROWS * 4))[lane];
+    const bool lab_ok = (p.label_filter == MRAG_LABEL_ANY) ? (lab >= 0) : (lab == p.label_filter);
+    const uint64_t tile_mask = __ballot(lab_ok);
     if (tile_mask != ~0ull) {
       mfma16_guard(acc[X]);
       const uint64_t lm = tile_mask >> (4 * g4);
@@ -675,10 +705,24 @@ __global__ __launch_bounds__(SCAN2_THREADS) void knn_scan3_kernel(ScanParams p) 
 #pragma unroll
       for (int qb = 0; qb < QB; ++qb) {
         if (theta_next[qb] != 0) theta_f[qb] = fmaxf(theta_f[qb], mrag_ord2f(theta_next[qb]));
-        asm volatile("" : "+v"(theta_f[qb]));
+        thr[qb] = fmaxf(ls[qb][KL3 - 1], theta_f[qb]);
+        asm volatile("" : "+v"(theta_f[qb]), "+v"(thr[qb]));
       }
     }
+    K7_STAMP(st2);
     __syncthreads();
+#ifdef MRAG_K7_STAMPS
+    K7_STAMP(st3);
+    if constexpr (QB == 4) {
+      st_sum[0] += st_mid - st0;
+      st_sum[1] += st1 - st_mid;
+    } else {
+      st_sum[1] += st1 - st0;
+    }
+    st_sum[2] += st2 - st1;
+    st_sum[3] += st3 - st2;
+    st_sum[4] += 1;
+#endif
   };
 
   if (my_tiles > 0) {
@@ -697,6 +741,13 @@ __global__ __launch_bounds__(SCAN2_THREADS) void knn_scan3_kernel(ScanParams p) 
       static_for<NGROUPS>([&](auto g_c) { epi_group(g_c, std::integral_constant<int, 1>{}); });
     }
   }
+#ifdef MRAG_K7_STAMPS
+  if constexpr (MODE == 0) {
+    const int wid = blockIdx.x * SCAN2_WAVES + w;
+    if (lane == 0 && wid < K7_MAXWAVES)
+      for (int i = 0; i < 5; ++i) g_k7_stamps[(size_t)wid * K7_NSTAMP + i] = st_sum[i];
+  }
+#endif
 
   if constexpr (MODE == 1) {
 #pragma unroll
@@ -1542,6 +1593,19 @@ int grow(mrag_knn_index* ix, int64_t need) {
 }  // namespace
 
 extern "C" {
+#ifdef MRAG_K7_STAMPS
+// diagnostic build only: copy the per-wave K7 segment sums of the last scan (n <= 2^16 * 8)
+__attribute__((visibility("default"))) int mrag_debug_k7_stamps(unsigned long long* out, int n) {
+  if (n > K7_MAXWAVES * K7_NSTAMP) n = K7_MAXWAVES * K7_NSTAMP;
+  MRAG_HIP(hipDeviceSynchronize());
+  MRAG_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_k7_stamps), (size_t)n * 8, 0, hipMemcpyDeviceToHost));
+  void* sym = nullptr;  // cleared for the next scan (waves it does not launch stay zero)
+  MRAG_HIP(hipGetSymbolAddress(&sym, HIP_SYMBOL(g_k7_stamps)));
+  MRAG_HIP(hipMemset(sym, 0, sizeof(g_k7_stamps)));
+  MRAG_HIP(hipDeviceSynchronize());
+  return MRAG_OK;
+}
+#endif
 
 int mrag_knn_create(int32_t dim, int32_t device, mrag_knn_index** out) {
   MRAG_REQUIRE(out != nullptr, "out is NULL");

@@ -50,7 +50,7 @@ with torch.cuda.stream(s):
     s.synchronize()
     dt1 = (time.perf_counter() - t0) / 200
     ms1, n1 = ix.profile(0)
-print(json.dumps({"env": {k: v for k, v in os.environ.items() if k.startswith("MRAG_")}, "scan_ms": round(ms / n, 4),
+print(json.dumps({"env": {k: os.path.basename(v) for k, v in os.environ.items() if k.startswith("MRAG_")}, "scan_ms": round(ms / n, 4),
                   "search_ms": round(dt * 1e3, 4), "tflops": round(2 * 1000 * (1 << 20) * 512 / (ms / n) / 1e9, 1),
                   "digest": digest, "uncertified": unc, "q1_search_ms": round(dt1 * 1e3, 4),
                   "q1_scan_ms": round(ms1 / n1, 4)}), flush=True)
