@@ -596,11 +596,13 @@ using mrag::static_for;
 // read_ag<b>): held as C++ values, 256 accumulator registers were copied and spilled
 #include "agpr_acc.inc"
 
-template <int EPI, int NS>
+// ABL (timing ablations, results wrong): 1 = no global loads, 2 = no ds_writes, 4 = no stores
+template <int EPI, int NS, int ABL = 0>
 __global__ __launch_bounds__(GF_THREADS, 1) void gemm_rs_kernel(GemmArgs g) {
   constexpr int BM = 256, BN = 256, WN = 128, NI = 8, NJ = 8;
   constexpr int A_BYTES = BM * 128, BUF = A_BYTES + BN * 128;
   constexpr int LA = BM * 8 / GF_THREADS, LT = 2 * LA;  // 16-byte chunks per thread per K-tile
+  constexpr int NA = 4;                                  // A-fragment ring (rows of 8 MFMAs)
   __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -627,6 +629,12 @@ __global__ __launch_bounds__(GF_THREADS, 1) void gemm_rs_kernel(GemmArgs g) {
   const __amdgpu_buffer_rsrc_t rW =
       __builtin_amdgcn_make_buffer_rsrc((void*)g.W, 0, (int)((int64_t)g.N * g.ldw * 2), 0x00020000);
   const uint32_t lds_st = (uint32_t)(s * 128 + ((c ^ ((s >> 1) & 7)) * 16));
+  // per-lane LDS pointers, one per buffer (and half), kept opaque so every access is base +
+  // 16-bit immediate: folded into one base, the buffer-1 offsets exceed the immediate and the
+  // compiler holds a separate address register per chunk / fragment (~30 VGPRs)
+  AS3 char* const lds0 = (AS3 char*)smem;
+  AS3 char* pS[2] = {lds0 + lds_st, lds0 + BUF + lds_st};
+  asm volatile("" : "+v"(pS[0]), "+v"(pS[1]));
   int ld_tile = 0, ld_kt = 0;  // the loader's position in this workgroup's K-tile stream
   uint32_t vA = 0, vW = 0;     // its per-thread byte offsets for the current tile
   auto ld_tile_origin = [&]() {
@@ -638,14 +646,19 @@ __global__ __launch_bounds__(GF_THREADS, 1) void gemm_rs_kernel(GemmArgs g) {
   ld_tile_origin();
   u32x4 R[NS][LT];
   auto load_ktile = [&](u32x4(&Rs)[LT]) {  // the loader's current K-tile into Rs, then advance
-    const int k0b = ld_kt * 128;
+    if constexpr ((ABL & 1) == 0) {
+      const int k0b = ld_kt * 128;
 #pragma unroll
-    for (int i = 0; i < LA; ++i)
-      Rs[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rA, vA, i * 32 * g.lda * 2 + k0b, 0));
+      for (int i = 0; i < LA; ++i)
+        Rs[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rA, vA, i * 32 * g.lda * 2 + k0b, 0));
 #pragma unroll
-    for (int i = 0; i < LA; ++i)
-      Rs[LA + i] =
-          __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rW, vW, i * 32 * g.ldw * 2 + k0b, 0));
+      for (int i = 0; i < LA; ++i)
+        Rs[LA + i] =
+            __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rW, vW, i * 32 * g.ldw * 2 + k0b, 0));
+    } else {
+#pragma unroll
+      for (int i = 0; i < LT; ++i) asm volatile("" : "+v"(Rs[i]));
+    }
     if (++ld_kt == ktiles) {
       ld_kt = 0;
       ++ld_tile;
@@ -653,42 +666,52 @@ __global__ __launch_bounds__(GF_THREADS, 1) void gemm_rs_kernel(GemmArgs g) {
     }
   };
   auto write_chunk = [&](const u32x4(&Rs)[LT], int buf, int i) {
-    const uint32_t base = (uint32_t)buf * BUF + (i < LA ? i * 4096 : A_BYTES + (i - LA) * 4096);
-    *(u32x4*)(smem + base + lds_st) = Rs[i];
+    if constexpr ((ABL & 2) == 0) *(AS3 u32x4*)(pS[buf] + (i < LA ? i * 4096 : A_BYTES + (i - LA) * 4096)) = Rs[i];
   };
 
   // fragments: A block i = LDS row 128 wr + 16 i + fr, W block jb = LDS row 128 wc + 16 jb + fr;
   // 32-deep half kk reads chunk 4 kk + fq, at position (4 kk + fq) ^ (fr >> 1)
-  uint32_t oA[2], oW[2];
+  AS3 char* pA[2][2];
+  AS3 char* pW[2][2];
 #pragma unroll
-  for (int kk = 0; kk < 2; ++kk) {
-    oA[kk] = (uint32_t)((128 * wr + fr) * 128 + (((4 * kk + fq) ^ (fr >> 1)) * 16));
-    oW[kk] = (uint32_t)(A_BYTES + (WN * wc + fr) * 128 + (((4 * kk + fq) ^ (fr >> 1)) * 16));
-  }
-  half8 fa[NI], fb0[NJ], fb1[NJ];
-  auto rdA = [&](int buf, int kk, int i) { return *(const half8*)(smem + buf * BUF + oA[kk] + i * 2048); };
-  auto rdW = [&](int buf, int kk, int jb) { return *(const half8*)(smem + buf * BUF + oW[kk] + jb * 2048); };
+  for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      pA[b][kk] = lds0 + b * BUF + (128 * wr + fr) * 128 + (((4 * kk + fq) ^ (fr >> 1)) * 16);
+      pW[b][kk] = lds0 + b * BUF + A_BYTES + (WN * wc + fr) * 128 + (((4 * kk + fq) ^ (fr >> 1)) * 16);
+      asm volatile("" : "+v"(pA[b][kk]), "+v"(pW[b][kk]));
+    }
+  // A rows r = 8 kk + i of a K-tile (row = the 8 MFMAs of block i, half kk) rotate through a ring
+  // of NA fragments: row r sits in fa[r % NA] and row r + NA is read right after row r's last MFMA
+  // (three rows = 24 MFMAs ahead of its use); the W fragments of the current half (fb0 / fb1)
+  // stay resident, the next half's are read during this one
+  half8 fa[NA], fb0[NJ], fb1[NJ];
+  auto rdA = [&](int buf, int kk, int i) { return *(const AS3 half8*)(pA[buf][kk] + i * 2048); };
+  auto rdW = [&](int buf, int kk, int jb) { return *(const AS3 half8*)(pW[buf][kk] + jb * 2048); };
 
   auto bar = [&]() {
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
   };
+  auto first_frags = [&]() {  // K-tile rows 0 .. NA - 1 and half 0's W fragments, from buffer 0
+#pragma unroll
+    for (int r = 0; r < NA; ++r) fa[r] = rdA(0, 0, r);
+#pragma unroll
+    for (int jb = 0; jb < NJ; ++jb) fb0[jb] = rdW(0, 0, jb);
+  };
 
-  // prologue: K-tile 0 into LDS buffer 0; K-tiles 1 .. NS in flight; K-tile 0's first-half fragments
+  // prologue: K-tile 0 into LDS buffer 0; K-tiles 1 .. NS in flight
   load_ktile(R[0]);
 #pragma unroll
   for (int i = 0; i < LT; ++i) write_chunk(R[0], 0, i);
 #pragma unroll
   for (int q = 1; q <= NS; ++q) load_ktile(R[q % NS]);
   bar();
-#pragma unroll
-  for (int i = 0; i < NI; ++i) fa[i] = rdA(0, 0, i);
-#pragma unroll
-  for (int jb = 0; jb < NJ; ++jb) fb0[jb] = rdW(0, 0, jb);
+  first_frags();
 
   // One K-tile t in LDS buffer X; set Rn holds K-tile t + 1 (written to buffer X ^ 1 in the first
-  // eight MFMA rows' gaps, two chunks per gap) and is then reloaded with K-tile t + 1 + NS. Every
+  // eight MFMA gaps, two chunks per gap) and is then reloaded with K-tile t + 1 + NS. Every
   // memory operation is unconditional (loads past the stream's end re-read the last tile, writes
   // past it go to a buffer nobody reads), so no register is merged across a branch. FIRST: the
   // tile's first K-tile (accumulators start at zero); LAST: its last (the next tile's first
@@ -696,38 +719,41 @@ __global__ __launch_bounds__(GF_THREADS, 1) void gemm_rs_kernel(GemmArgs g) {
   auto ktile = [&](auto x_c, auto first_c, auto last_c, u32x4(&Rn)[LT]) {
     constexpr int X = decltype(x_c)::value;
     constexpr bool FIRST = decltype(first_c)::value, LAST = decltype(last_c)::value;
-    static_for<NI>([&](auto i_c) {
-      constexpr int i = decltype(i_c)::value;
-      static_for<NJ>([&](auto jb_c) {
-        constexpr int jb = decltype(jb_c)::value;
-        if constexpr (FIRST)
-          mfma_ag0<i * NJ + jb>(fb0[jb], fa[i]);
-        else
-          mfma_ag<i * NJ + jb>(fb0[jb], fa[i]);
-        constexpr int gap = i * NJ + jb;
-        if constexpr (gap < LT / 2) {  // the next K-tile into LDS, two chunks per gap
-          write_chunk(Rn, X ^ 1, 2 * gap);
-          write_chunk(Rn, X ^ 1, 2 * gap + 1);
-        } else if constexpr (gap == LT / 2) {
-          load_ktile(Rn);
-        } else if constexpr (gap > LT / 2 && gap <= LT / 2 + NJ) {
-          fb1[gap - LT / 2 - 1] = rdW(X, 1, gap - LT / 2 - 1);
-        }
-        if constexpr (jb == NJ - 1) fa[i] = rdA(X, 1, i);  // fa[i]'s last first-half use
-        __builtin_amdgcn_sched_barrier(0);
-      });
-    });
-    bar();
-    static_for<NI>([&](auto i_c) {
-      constexpr int i = decltype(i_c)::value;
-      static_for<NJ>([&](auto jb_c) {
-        constexpr int jb = decltype(jb_c)::value;
-        mfma_ag<i * NJ + jb>(fb1[jb], fa[i]);
-        if constexpr (!LAST) {
-          if constexpr (i == 0) fb0[jb] = rdW(X ^ 1, 0, jb);
-          if constexpr (jb == NJ - 1) fa[i] = rdA(X ^ 1, 0, i);
-        }
-        __builtin_amdgcn_sched_barrier(0);
+    static_for<2>([&](auto kk_c) {
+      constexpr int kk = decltype(kk_c)::value;
+      if constexpr (kk == 1) bar();
+      static_for<NI>([&](auto i_c) {
+        constexpr int i = decltype(i_c)::value;
+        constexpr int r = 8 * kk + i;  // this row; row r + NA goes into its slot afterwards
+        static_for<NJ>([&](auto jb_c) {
+          constexpr int jb = decltype(jb_c)::value;
+          const half8& wf = kk == 0 ? fb0[jb] : fb1[jb];
+          if constexpr (FIRST && kk == 0)
+            mfma_ag0<i * NJ + jb>(wf, fa[r % NA]);
+          else
+            mfma_ag<i * NJ + jb>(wf, fa[r % NA]);
+          constexpr int gap = i * NJ + jb;
+          if constexpr (kk == 0) {
+            if constexpr (gap < LT / 2) {  // the next K-tile into LDS, two chunks per gap
+              write_chunk(Rn, X ^ 1, 2 * gap);
+              write_chunk(Rn, X ^ 1, 2 * gap + 1);
+            } else if constexpr (gap == LT / 2) {
+              load_ktile(Rn);
+            } else if constexpr (gap > LT / 2 && gap <= LT / 2 + NJ) {
+              fb1[gap - LT / 2 - 1] = rdW(X, 1, gap - LT / 2 - 1);
+            }
+          } else if constexpr (!LAST && i == 0) {
+            fb0[jb] = rdW(X ^ 1, 0, jb);  // after the barrier: K-tile t + 1 is in buffer X ^ 1
+          }
+          if constexpr (jb == NJ - 1) {
+            constexpr int rn = r + NA;
+            if constexpr (rn < 16)
+              fa[r % NA] = rdA(X, rn >> 3, rn & 7);
+            else if constexpr (!LAST)
+              fa[r % NA] = rdA(X ^ 1, 0, rn - 16);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        });
       });
     });
   };
@@ -773,14 +799,10 @@ __global__ __launch_bounds__(GF_THREADS, 1) void gemm_rs_kernel(GemmArgs g) {
         constexpr int i = decltype(i_c)::value;
         const int m = m0 + 128 * wr + 16 * i + fr;
         const f32x4 v0 = read_ag<i * NJ + 2 * p>(), v1 = read_ag<i * NJ + 2 * p + 1>();
-        if (m < g.M) gemm_store8<EPI>(g, m, n, v0, v1, bn);
+        if ((ABL & 4) == 0 && m < g.M) gemm_store8<EPI>(g, m, n, v0, v1, bn);
       });
     });
-    // the next tile's first fragments (its K-tile 0 is in LDS buffer 0)
-#pragma unroll
-    for (int i = 0; i < NI; ++i) fa[i] = rdA(0, 0, i);
-#pragma unroll
-    for (int jb = 0; jb < NJ; ++jb) fb0[jb] = rdW(0, 0, jb);
+    first_frags();  // the next tile's K-tile 0 is in LDS buffer 0
   }
 }
 
@@ -1267,10 +1289,18 @@ template <int EPI>
 struct K3fKern2 {
   static constexpr auto fn = gemm_rs_kernel<EPI, 2>;
 };
-// env MRAG_GEMM_K3F (experiment): 1 / 2 = K3f with one / two staging sets where K3d would run
+// env MRAG_GEMM_K3F (experiment): 1 / 2 = K3f with one / two staging sets where K3d would run;
+// MRAG_K3F_ABL = ablation bits (timing only, f16-output GEMMs, two sets)
 int k3f_mode() {
   static const int v = [] {
     const char* e = getenv("MRAG_GEMM_K3F");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+int k3f_abl() {
+  static const int v = [] {
+    const char* e = getenv("MRAG_K3F_ABL");
     return e ? atoi(e) : 0;
   }();
   return v;
@@ -1282,6 +1312,18 @@ int launch_gemm(const GemmArgs& g, int epi, hipStream_t s) {
       (int64_t)g.N * g.ldw * 2 < (1ll << 31) && g.lda % 8 == 0 && g.ldw % 8 == 0 && g.ldc % 4 == 0) {
     const int ntiles = ((g.M + 255) / 256) * (g.N / 256);
     const int nb = std::min((ntiles + 7) / 8 * 8, std::max(8, num_cus() / 8 * 8));
+    if (k3f_abl() != 0 && epi == EPI_F16) {
+      const dim3 grid((unsigned)nb), block(GF_THREADS);
+      switch (k3f_abl()) {
+        case 1: hipLaunchKernelGGL((gemm_rs_kernel<EPI_F16, 2, 1>), grid, block, 0, s, g); break;
+        case 2: hipLaunchKernelGGL((gemm_rs_kernel<EPI_F16, 2, 2>), grid, block, 0, s, g); break;
+        case 3: hipLaunchKernelGGL((gemm_rs_kernel<EPI_F16, 2, 3>), grid, block, 0, s, g); break;
+        case 4: hipLaunchKernelGGL((gemm_rs_kernel<EPI_F16, 2, 4>), grid, block, 0, s, g); break;
+        default: hipLaunchKernelGGL((gemm_rs_kernel<EPI_F16, 2, 7>), grid, block, 0, s, g); break;
+      }
+      MRAG_CHECK_LAUNCH();
+      return MRAG_OK;
+    }
     return k3f_mode() == 2 ? launch_epi<K3fKern2>(epi, dim3((unsigned)nb), dim3(GF_THREADS), s, g)
                            : launch_epi<K3fKern1>(epi, dim3((unsigned)nb), dim3(GF_THREADS), s, g);
   }
