@@ -571,242 +571,6 @@ __global__ __launch_bounds__(G8_THREADS) void gemm_8p_kernel(GemmArgs g) {
 }
 
 // ---------------------------------------------------------------------------
-// K3f (M >= 1024, experiment behind MRAG_GEMM_K3F): persistent, one workgroup of FOUR waves per
-// CU (2 x 2, one per SIMD), 256 x 256 tiles (waves of 128 x 128, the accumulators in AGPRs),
-// 64-deep K-tiles double-buffered in LDS, operands staged through VGPRs (buffer_load_dwordx4 ->
-// ds_write_b128) with NS staging sets: K-tile t writes K-tile t + 1 into the other LDS buffer in
-// its first quarter and reloads that set with K-tile t + 1 + NS, so a load has NS - 1/2 K-tiles
-// of MFMAs to land before its ds_write.
-//  * per K-tile a wave issues 128 MFMA 16x16x32 (8 x 8 blocks over two 32-deep halves); a
-//    fragment of the next half is read right after the last MFMA that uses its register; one
-//    barrier per K-tile, between the halves: before it every wave's ds_writes of K-tile t + 1 and
-//    its reads of K-tile t are done, after it the second half reads K-tile t + 1's first-half
-//    fragments only;
-//  * rows past M read as zero (buffer range check) and are never stored; chunk c of LDS row j sits
-//    at c ^ ((j >> 1) & 7) (conflict-free ds_read_b128, as K3 / K3d);
-//  * weight rows are permuted in LDS (g8_colperm) so a lane's two 16 x 16 blocks of a pair hold 8
-//    consecutive output columns: gemm_store8, the same per-element accumulation order (32-deep
-//    chunks, ascending k, one accumulator) and epilogue as K3 / K3d: bit-identical results;
-//  * tiles: XCD x owns a contiguous range of tile ids (tm-major), dealt round-robin to its
-//    workgroups, so a 256-row activation panel stays in that XCD's L2.
-constexpr int GF_THREADS = 256;
-using mrag::static_for;
-
-// accumulator block b of a wave lives in a[4 b : 4 b + 3] (mfma_ag<b> / mfma_ag0<b> from zero /
-// read_ag<b>): held as C++ values, 256 accumulator registers were copied and spilled
-#include "agpr_acc.inc"
-
-// ABL (timing ablations, results wrong): 1 = no global loads, 2 = no ds_writes, 4 = no stores
-template <int EPI, int NS, int ABL = 0>
-__global__ __launch_bounds__(GF_THREADS, 1) void gemm_rs_kernel(GemmArgs g) {
-  constexpr int BM = 256, BN = 256, WN = 128, NI = 8, NJ = 8;
-  constexpr int A_BYTES = BM * 128, BUF = A_BYTES + BN * 128;
-  constexpr int LA = BM * 8 / GF_THREADS, LT = 2 * LA;  // 16-byte chunks per thread per K-tile
-  constexpr int NA = 4;                                  // A-fragment ring (rows of 8 MFMAs)
-  __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = w >> 1, wc = w & 1;
-  const int fr = lane & 15, fq = lane >> 4;
-
-  const int tiles_n = g.N / BN;
-  const int ntiles = ((g.M + BM - 1) / BM) * tiles_n;
-  const int xcd = blockIdx.x & 7, sidx = blockIdx.x >> 3;
-  const int nbx = ((int)gridDim.x - xcd + 7) >> 3;
-  const int q8 = ntiles >> 3, r8 = ntiles & 7;
-  const int lo = xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8;
-  const int cnt = q8 + (xcd < r8 ? 1 : 0);
-  const int my_n = sidx < cnt ? (cnt - sidx + nbx - 1) / nbx : 0;
-  if (my_n == 0) return;  // whole workgroup, before any barrier
-  const int ktiles = g.K / 64;  // even, >= 4 (launcher)
-
-  // staging: thread tid loads chunk c = tid & 7 of LDS rows 32 i + s (s = tid >> 3): A row
-  // m0 + that row, W row n0 + 32 i + g8_colperm(s) (the column that LDS row holds)
-  const int s = tid >> 3, c = tid & 7;
-  const __amdgpu_buffer_rsrc_t rA =
-      __builtin_amdgcn_make_buffer_rsrc((void*)g.A, 0, (int)((int64_t)g.M * g.lda * 2), 0x00020000);
-  const __amdgpu_buffer_rsrc_t rW =
-      __builtin_amdgcn_make_buffer_rsrc((void*)g.W, 0, (int)((int64_t)g.N * g.ldw * 2), 0x00020000);
-  const uint32_t lds_st = (uint32_t)(s * 128 + ((c ^ ((s >> 1) & 7)) * 16));
-  // per-lane LDS pointers, one per buffer (and half), kept opaque so every access is base +
-  // 16-bit immediate: folded into one base, the buffer-1 offsets exceed the immediate and the
-  // compiler holds a separate address register per chunk / fragment (~30 VGPRs)
-  AS3 char* const lds0 = (AS3 char*)smem;
-  AS3 char* pS[2] = {lds0 + lds_st, lds0 + BUF + lds_st};
-  asm volatile("" : "+v"(pS[0]), "+v"(pS[1]));
-  int ld_tile = 0, ld_kt = 0;  // the loader's position in this workgroup's K-tile stream
-  uint32_t vA = 0, vW = 0;     // its per-thread byte offsets for the current tile
-  auto ld_tile_origin = [&]() {
-    const int T = lo + sidx + min(ld_tile, my_n - 1) * nbx;  // past the end: re-read the last tile
-    const int tm = T / tiles_n;
-    vA = (uint32_t)((tm * BM + s) * g.lda * 2 + c * 16);
-    vW = (uint32_t)(((T - tm * tiles_n) * BN + g8_colperm(s)) * g.ldw * 2 + c * 16);
-  };
-  ld_tile_origin();
-  u32x4 R[NS][LT];
-  auto load_ktile = [&](u32x4(&Rs)[LT]) {  // the loader's current K-tile into Rs, then advance
-    if constexpr ((ABL & 1) == 0) {
-      const int k0b = ld_kt * 128;
-#pragma unroll
-      for (int i = 0; i < LA; ++i)
-        Rs[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rA, vA, i * 32 * g.lda * 2 + k0b, 0));
-#pragma unroll
-      for (int i = 0; i < LA; ++i)
-        Rs[LA + i] =
-            __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rW, vW, i * 32 * g.ldw * 2 + k0b, 0));
-    } else {
-#pragma unroll
-      for (int i = 0; i < LT; ++i) asm volatile("" : "+v"(Rs[i]));
-    }
-    if (++ld_kt == ktiles) {
-      ld_kt = 0;
-      ++ld_tile;
-      ld_tile_origin();
-    }
-  };
-  auto write_chunk = [&](const u32x4(&Rs)[LT], int buf, int i) {
-    if constexpr ((ABL & 2) == 0) *(AS3 u32x4*)(pS[buf] + (i < LA ? i * 4096 : A_BYTES + (i - LA) * 4096)) = Rs[i];
-  };
-
-  // fragments: A block i = LDS row 128 wr + 16 i + fr, W block jb = LDS row 128 wc + 16 jb + fr;
-  // 32-deep half kk reads chunk 4 kk + fq, at position (4 kk + fq) ^ (fr >> 1)
-  AS3 char* pA[2][2];
-  AS3 char* pW[2][2];
-#pragma unroll
-  for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-    for (int b = 0; b < 2; ++b) {
-      pA[b][kk] = lds0 + b * BUF + (128 * wr + fr) * 128 + (((4 * kk + fq) ^ (fr >> 1)) * 16);
-      pW[b][kk] = lds0 + b * BUF + A_BYTES + (WN * wc + fr) * 128 + (((4 * kk + fq) ^ (fr >> 1)) * 16);
-      asm volatile("" : "+v"(pA[b][kk]), "+v"(pW[b][kk]));
-    }
-  // A rows r = 8 kk + i of a K-tile (row = the 8 MFMAs of block i, half kk) rotate through a ring
-  // of NA fragments: row r sits in fa[r % NA] and row r + NA is read right after row r's last MFMA
-  // (three rows = 24 MFMAs ahead of its use); the W fragments of the current half (fb0 / fb1)
-  // stay resident, the next half's are read during this one
-  half8 fa[NA], fb0[NJ], fb1[NJ];
-  auto rdA = [&](int buf, int kk, int i) { return *(const AS3 half8*)(pA[buf][kk] + i * 2048); };
-  auto rdW = [&](int buf, int kk, int jb) { return *(const AS3 half8*)(pW[buf][kk] + jb * 2048); };
-
-  auto bar = [&]() {
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-  };
-  auto first_frags = [&]() {  // K-tile rows 0 .. NA - 1 and half 0's W fragments, from buffer 0
-#pragma unroll
-    for (int r = 0; r < NA; ++r) fa[r] = rdA(0, 0, r);
-#pragma unroll
-    for (int jb = 0; jb < NJ; ++jb) fb0[jb] = rdW(0, 0, jb);
-  };
-
-  // prologue: K-tile 0 into LDS buffer 0; K-tiles 1 .. NS in flight
-  load_ktile(R[0]);
-#pragma unroll
-  for (int i = 0; i < LT; ++i) write_chunk(R[0], 0, i);
-#pragma unroll
-  for (int q = 1; q <= NS; ++q) load_ktile(R[q % NS]);
-  bar();
-  first_frags();
-
-  // One K-tile t in LDS buffer X; set Rn holds K-tile t + 1 (written to buffer X ^ 1 in the first
-  // eight MFMA gaps, two chunks per gap) and is then reloaded with K-tile t + 1 + NS. Every
-  // memory operation is unconditional (loads past the stream's end re-read the last tile, writes
-  // past it go to a buffer nobody reads), so no register is merged across a branch. FIRST: the
-  // tile's first K-tile (accumulators start at zero); LAST: its last (the next tile's first
-  // fragments are read after the epilogue).
-  auto ktile = [&](auto x_c, auto first_c, auto last_c, u32x4(&Rn)[LT]) {
-    constexpr int X = decltype(x_c)::value;
-    constexpr bool FIRST = decltype(first_c)::value, LAST = decltype(last_c)::value;
-    static_for<2>([&](auto kk_c) {
-      constexpr int kk = decltype(kk_c)::value;
-      if constexpr (kk == 1) bar();
-      static_for<NI>([&](auto i_c) {
-        constexpr int i = decltype(i_c)::value;
-        constexpr int r = 8 * kk + i;  // this row; row r + NA goes into its slot afterwards
-        static_for<NJ>([&](auto jb_c) {
-          constexpr int jb = decltype(jb_c)::value;
-          const half8& wf = kk == 0 ? fb0[jb] : fb1[jb];
-          if constexpr (FIRST && kk == 0)
-            mfma_ag0<i * NJ + jb>(wf, fa[r % NA]);
-          else
-            mfma_ag<i * NJ + jb>(wf, fa[r % NA]);
-          constexpr int gap = i * NJ + jb;
-          if constexpr (kk == 0) {
-            if constexpr (gap < LT / 2) {  // the next K-tile into LDS, two chunks per gap
-              write_chunk(Rn, X ^ 1, 2 * gap);
-              write_chunk(Rn, X ^ 1, 2 * gap + 1);
-            } else if constexpr (gap == LT / 2) {
-              load_ktile(Rn);
-            } else if constexpr (gap > LT / 2 && gap <= LT / 2 + NJ) {
-              fb1[gap - LT / 2 - 1] = rdW(X, 1, gap - LT / 2 - 1);
-            }
-          } else if constexpr (!LAST && i == 0) {
-            fb0[jb] = rdW(X ^ 1, 0, jb);  // after the barrier: K-tile t + 1 is in buffer X ^ 1
-          }
-          if constexpr (jb == NJ - 1) {
-            constexpr int rn = r + NA;
-            if constexpr (rn < 16)
-              fa[r % NA] = rdA(X, rn >> 3, rn & 7);
-            else if constexpr (!LAST)
-              fa[r % NA] = rdA(X ^ 1, 0, rn - 16);
-          }
-          __builtin_amdgcn_sched_barrier(0);
-        });
-      });
-    });
-  };
-  using F = std::false_type;
-  using Tr = std::true_type;
-  using X0 = std::integral_constant<int, 0>;
-  using X1 = std::integral_constant<int, 1>;
-  // K-tile t of the stream writes set (t + 1) % NS; ktiles is even and NS divides 2, so every
-  // tile starts in LDS buffer 0 with the same set pattern
-  auto& Ra = R[1 % NS];
-  auto& Rb = R[0];
-  for (int tile_i = 0; tile_i < my_n; ++tile_i) {
-    ktile(X0{}, Tr{}, F{}, Ra);
-    ktile(X1{}, F{}, F{}, Rb);
-    for (int kt = 2; kt < ktiles - 2; kt += 2) {
-      ktile(X0{}, F{}, F{}, Ra);
-      ktile(X1{}, F{}, F{}, Rb);
-    }
-    ktile(X0{}, F{}, F{}, Ra);
-    ktile(X1{}, F{}, Tr{}, Rb);
-    // epilogue: the MFMAs are asm, so the hazard recognizer cannot space the accumulator reads
-    // from them: let the last ones retire first
-    asm volatile("s_nop 15\n\ts_nop 3" ::: "memory");
-    const int T = lo + sidx + tile_i * nbx;
-    const int tm = T / tiles_n;
-    const int m0 = tm * BM, n0 = (T - tm * tiles_n) * BN;
-    static_for<NJ / 2>([&](auto p_c) {
-      constexpr int p = decltype(p_c)::value;
-      const int n = n0 + WN * wc + 32 * p + 8 * fq;
-      float bn[8];
-      if (g.bias) {
-        const f32x4 b0 = *(const f32x4*)(g.bias + n), b1 = *(const f32x4*)(g.bias + n + 4);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          bn[r] = b0[r];
-          bn[4 + r] = b1[r];
-        }
-      } else {
-#pragma unroll
-        for (int r = 0; r < 8; ++r) bn[r] = 0.f;
-      }
-      static_for<NI>([&](auto i_c) {
-        constexpr int i = decltype(i_c)::value;
-        const int m = m0 + 128 * wr + 16 * i + fr;
-        const f32x4 v0 = read_ag<i * NJ + 2 * p>(), v1 = read_ag<i * NJ + 2 * p + 1>();
-        if ((ABL & 4) == 0 && m < g.M) gemm_store8<EPI>(g, m, n, v0, v1, bn);
-      });
-    });
-    first_frags();  // the next tile's K-tile 0 is in LDS buffer 0
-  }
-}
-
-// ---------------------------------------------------------------------------
 // K2: LayerNorm over rows of D <= 1024 (one wave per row, two-pass mean/var in f32).
 // Optional row gather (pooling), f32 and/or f16 outputs (in-place f32 allowed).
 __global__ __launch_bounds__(256) void layernorm_kernel(LayerNormArgs a) {
@@ -1281,52 +1045,8 @@ struct K3Kern {
   static constexpr auto fn = gemm_nt_kernel<EPI>;
 };
 
-template <int EPI>
-struct K3fKern1 {
-  static constexpr auto fn = gemm_rs_kernel<EPI, 1>;
-};
-template <int EPI>
-struct K3fKern2 {
-  static constexpr auto fn = gemm_rs_kernel<EPI, 2>;
-};
-// env MRAG_GEMM_K3F (experiment): 1 / 2 = K3f with one / two staging sets where K3d would run;
-// MRAG_K3F_ABL = ablation bits (timing only, f16-output GEMMs, two sets)
-int k3f_mode() {
-  static const int v = [] {
-    const char* e = getenv("MRAG_GEMM_K3F");
-    return e ? atoi(e) : 0;
-  }();
-  return v;
-}
-int k3f_abl() {
-  static const int v = [] {
-    const char* e = getenv("MRAG_K3F_ABL");
-    return e ? atoi(e) : 0;
-  }();
-  return v;
-}
-
 int launch_gemm(const GemmArgs& g, int epi, hipStream_t s) {
   if (g.M <= 0) return MRAG_OK;
-  if (k3f_mode() != 0 && g.M >= 1024 && g.N % 256 == 0 && g.K % 128 == 0 && g.K >= 256 && (int64_t)g.M * g.lda * 2 < (1ll << 31) &&
-      (int64_t)g.N * g.ldw * 2 < (1ll << 31) && g.lda % 8 == 0 && g.ldw % 8 == 0 && g.ldc % 4 == 0) {
-    const int ntiles = ((g.M + 255) / 256) * (g.N / 256);
-    const int nb = std::min((ntiles + 7) / 8 * 8, std::max(8, num_cus() / 8 * 8));
-    if (k3f_abl() != 0 && epi == EPI_F16) {
-      const dim3 grid((unsigned)nb), block(GF_THREADS);
-      switch (k3f_abl()) {
-        case 1: hipLaunchKernelGGL((gemm_rs_kernel<EPI_F16, 2, 1>), grid, block, 0, s, g); break;
-        case 2: hipLaunchKernelGGL((gemm_rs_kernel<EPI_F16, 2, 2>), grid, block, 0, s, g); break;
-        case 3: hipLaunchKernelGGL((gemm_rs_kernel<EPI_F16, 2, 3>), grid, block, 0, s, g); break;
-        case 4: hipLaunchKernelGGL((gemm_rs_kernel<EPI_F16, 2, 4>), grid, block, 0, s, g); break;
-        default: hipLaunchKernelGGL((gemm_rs_kernel<EPI_F16, 2, 7>), grid, block, 0, s, g); break;
-      }
-      MRAG_CHECK_LAUNCH();
-      return MRAG_OK;
-    }
-    return k3f_mode() == 2 ? launch_epi<K3fKern2>(epi, dim3((unsigned)nb), dim3(GF_THREADS), s, g)
-                           : launch_epi<K3fKern1>(epi, dim3((unsigned)nb), dim3(GF_THREADS), s, g);
-  }
   MRAG_REQUIRE(g.N % GN == 0 && g.K % GK == 0, "gemm: N=%d must be a multiple of %d and K=%d of %d", g.N, GN, g.K,
                GK);
   MRAG_REQUIRE(g.lda % 8 == 0 && g.ldw % 8 == 0 && g.ldc % 4 == 0, "gemm: lda/ldw must be multiples of 8, ldc of 4");
