@@ -50,11 +50,17 @@ def _dist_setup():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one process per GPU; more ranks than GPUs (a rehearsal of the N > 1 path on a smaller box,
+    # MRAG_DIST_BACKEND=gloo) share them round-robin. device_count() does not initialise the GPU.
+    local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        backend = os.environ.get("MRAG_DIST_BACKEND", "nccl")  # "nccl" is RCCL on ROCm
+        if backend == "nccl":
+            dist.init_process_group(backend, device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     return world, rank, local
 
 
@@ -439,8 +445,13 @@ def fusion_leg(world: int, rank: int, local: int, steps: int, warmup: int):
             return v
         buf = torch.zeros((per, v.shape[1]), dtype=v.dtype, device=dev)
         buf[: v.shape[0]] = v
-        out = torch.empty((world * per, v.shape[1]), dtype=v.dtype, device=dev)
-        dist.all_gather_into_tensor(out, buf)
+        if dist.get_backend() == "nccl":
+            out = torch.empty((world * per, v.shape[1]), dtype=v.dtype, device=dev)
+            dist.all_gather_into_tensor(out, buf)
+        else:  # gloo rehearsal
+            parts = [torch.empty_like(buf) for _ in range(world)]
+            dist.all_gather(parts, buf)
+            out = torch.cat(parts)
         return out[:NQ]
 
     # The leg runs on its own streams: device-pointer encoder calls are then stream-ordered (no
