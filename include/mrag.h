@@ -21,6 +21,10 @@
  *   - plain pointers and sizes only; `ptr_kind` says whether data pointers are
  *     host (MRAG_PTR_HOST) or device (MRAG_PTR_DEVICE) memory;
  *   - `stream` is a hipStream_t passed as void* (NULL = the handle's stream);
+ *     device-pointer inputs with stream == NULL are read after the work already
+ *     queued on the legacy NULL stream (an event on stream 0 orders the handle's
+ *     stream behind it), so data a caller produced with default-stream kernels or
+ *     copies is complete when the library reads it;
  *   - handles are opaque; calls on one handle are serialised by an internal
  *     mutex, so a handle may be used from any single thread at a time.
  */
