@@ -693,6 +693,39 @@ __global__ __launch_bounds__(256) void layernorm4_kernel(LayerNormArgs a) {
            a.y16 ? a.y16 + (size_t)r * a.D : nullptr);
 }
 
+// K2 streaming form (the same arithmetic, bit-identical to layernorm4_kernel): a persistent grid
+// of LN_WG_PER_CU workgroups per CU; a wave walks rows w, w + W, ... (W = the grid's waves),
+// loads its gamma / beta chunks once and issues the next row's loads before this row's
+// reductions, so each wave keeps a row in flight while it reduces the previous one (one row per
+// wave left every wave waiting on its own loads: ViT LayerNorm 13.6 -> 11.7 us; 2 and 8
+// workgroups per CU measured 13.4 / 12.6 us).
+constexpr int LN_WG_PER_CU = 4;
+__global__ __launch_bounds__(256) void layernorm_stream_kernel(LayerNormArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int nw = (int)gridDim.x * 4;
+  int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= a.rows) return;
+  const int nc = a.D >> 2;
+  f32x4 g4[4], b4[4];
+  ln_params4(lane, a.D, a.gamma, a.beta, g4, b4);
+  auto load = [&](int row, f32x4(&v)[4]) {
+    const int src = a.gather ? a.gather[row] : row;
+    const f32x4* x = (const f32x4*)(a.x + (size_t)src * a.ldx);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = lane + 64 * j < nc ? x[lane + 64 * j] : f32x4{};
+  };
+  f32x4 v[4], vn[4];
+  load(r, v);
+  for (; r < a.rows; r += nw) {
+    const int rn = r + nw;
+    if (rn < a.rows) load(rn, vn);
+    ln_row4p(v, lane, a.D, a.eps, g4, b4, a.y32 ? a.y32 + (size_t)r * a.D : nullptr,
+             a.y16 ? a.y16 + (size_t)r * a.D : nullptr);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = vn[j];
+  }
+}
+
 // ViT token assembly + pre_layrnorm in one pass (modeling_clip.py:212-217, :642):
 // X[b*T + t] = LN((t == 0 ? cls : patch[b*(T-1) + t-1]) + pos[t])   (f32)
 __global__ __launch_bounds__(256) void vit_embed_ln_kernel(const float* __restrict__ patch,
@@ -1064,7 +1097,12 @@ int launch_layernorm(const LayerNormArgs& a, hipStream_t s) {
   MRAG_REQUIRE(a.D > 0 && a.D <= 1024, "layernorm: D=%d unsupported", a.D);
   const bool vec4 = a.D % 4 == 0 && a.ldx % 4 == 0 && ((uintptr_t)a.x & 15) == 0 && ((uintptr_t)a.gamma & 15) == 0 &&
                     ((uintptr_t)a.beta & 15) == 0 && ((uintptr_t)a.y32 & 15) == 0 && ((uintptr_t)a.y16 & 7) == 0;
-  if (vec4)
+  // in place through a gather, two output rows could read one input row another wave overwrites
+  const bool alias = a.gather && a.y32 == a.x;
+  if (vec4 && !alias) {
+    const int nb = std::min((a.rows + 3) / 4, num_cus() * LN_WG_PER_CU);
+    hipLaunchKernelGGL(layernorm_stream_kernel, dim3((unsigned)nb), dim3(256), 0, s, a);
+  } else if (vec4)
     hipLaunchKernelGGL(layernorm4_kernel, dim3((unsigned)((a.rows + 3) / 4)), dim3(256), 0, s, a);
   else
     hipLaunchKernelGGL(layernorm_kernel, dim3((unsigned)((a.rows + 3) / 4)), dim3(256), 0, s, a);
