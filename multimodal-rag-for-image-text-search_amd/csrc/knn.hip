@@ -509,6 +509,9 @@ __global__ __launch_bounds__(SCAN2_THREADS) void knn_scan3_kernel(ScanParams p) 
   }
   uint32_t* const theta_q = p.theta + slot0;
   const bool may_publish = p.k <= KL3;
+  // row validity in one compare: (unsigned)(label - lo) <= span (ANY: label >= 0; else equality)
+  const int lab_lo = p.label_filter == MRAG_LABEL_ANY ? 0 : p.label_filter;
+  const uint32_t lab_span = p.label_filter == MRAG_LABEL_ANY ? 0x7fffffffu : 0u;
 
   // A fragment of row 16 rb + c16, chunk 4 kk + g4, sits at chunk (4 kk + g4) ^ c16: byte
   // offset (offA0 ^ ((kk & 3) << 6)) + (kk >> 2) * 256 + rb * 16 * ROW_BYTES
@@ -568,7 +571,12 @@ __global__ __launch_bounds__(SCAN2_THREADS) void knn_scan3_kernel(ScanParams p) 
       asm volatile("v_max_f32 %0, %0, %1" : "+v"(sm) : "v"(gm));
       smax[qb] = sm;
     } else {
+#ifdef MRAG_K7_ABL_NOINS
+      // timing ablation only (results wrong): no group test ever fires
+      if (__any(gm > thr[qb]) && p.k < 0) {
+#else
       if (__any(gm > thr[qb])) {
+#endif
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const float sv = av[r];
@@ -595,10 +603,14 @@ __global__ __launch_bounds__(SCAN2_THREADS) void knn_scan3_kernel(ScanParams p) 
     const char* gw = (const char*)p.x16 + (size_t)ntile * TILE_BYTES + (size_t)w * GLDS_PER_WAVE * ROW_BYTES;
     uint32_t ldsw = lds_base + Y * TILE_BYTES + w * GLDS_PER_WAVE * 1024;
     asm volatile("" : "+s"(gw), "+s"(ldsw));
+    // the shared threshold only moves when lanes publish (k <= KL3); otherwise the seed read
+    // before the loop stays exact and no tile pays the reloads or their tail update
     if constexpr (MODE == 0) {
+      if (may_publish) {
 #pragma unroll
-      for (int qb = 0; qb < QB; ++qb)
-        theta_next[qb] = __hip_atomic_load(theta_q + 16 * qb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (int qb = 0; qb < QB; ++qb)
+          theta_next[qb] = __hip_atomic_load(theta_q + 16 * qb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
     const char* tb = smem + X * TILE_BYTES;
     int lane_t = lane, offA0 = offA0_init;
@@ -622,6 +634,12 @@ __global__ __launch_bounds__(SCAN2_THREADS) void knn_scan3_kernel(ScanParams p) 
 #pragma unroll
     for (int n = 0; n < NA; ++n) read_a(n >> 2, n & 3);
     stage_labels(Y, ntile);
+    // QB = 4: the tile's row-validity mask is built in the MFMA gaps (label read at k-step KLAB,
+    // ballot one k-step later; buffer X's labels are not rewritten before the end-of-tile barrier),
+    // so the tile tail holds only a wave-uniform test of it
+    constexpr int KLAB = KSTEPS / 2 - 1;
+    int lab_v = 0;
+    uint64_t tile_mask = ~0ull;
     if constexpr (QB == 1) {
       // K7s (fill-bound): every piece of the next tile at the top of the tile, so the DMA has the
       // whole tile to land; per k-step the four row blocks' MFMAs, each followed by its next
@@ -662,6 +680,9 @@ __global__ __launch_bounds__(SCAN2_THREADS) void knn_scan3_kernel(ScanParams p) 
             voff = (lane16 ^ (uint32_t)(pc << 4)) + (uint32_t)(pc * 1024);
             asm volatile("s_mov_b32 m0, %1" : "+v"(voff) : "s"(ldsw + pc * 1024));
           }
+          static_assert(KLAB * FRONT >= GLDS_PER_WAVE, "label slots must follow the DMA k-steps");
+          if constexpr (kk == KLAB && j == 1) lab_v = ((const int*)(smem + LBL_OFF + X * TILE_ROWS * 4))[lane];
+          if constexpr (kk == KLAB + 1 && j == 1) tile_mask = __ballot((uint32_t)(lab_v - lab_lo) <= lab_span);
         } else if constexpr ((j & 3) == 2) {  // ... and its DMA
           constexpr int pc = FRONT * kk + (j >> 2);
           if constexpr ((j >> 2) < FRONT && pc < GLDS_PER_WAVE) {
@@ -682,11 +703,12 @@ __global__ __launch_bounds__(SCAN2_THREADS) void knn_scan3_kernel(ScanParams p) 
     });
     K7_STAMP(st1);
     if constexpr (CPR == 64 && QB == 4) asm volatile("s_mov_b32 m0, %0" ::"s"(m0_keep));
-    // the tile's labels, read after its MFMAs (a read at the top would wait for its LDS
-    // round trip before the first MFMA; buffer X is not rewritten before the barrier)
-    const int lab = ((const int*)(smem + LBL_OFF + X * TILE_ROWS * 4))[lane];
-    const bool lab_ok = (p.label_filter == MRAG_LABEL_ANY) ? (lab >= 0) : (lab == p.label_filter);
-    const uint64_t tile_mask = __ballot(lab_ok);
+    if constexpr (QB == 1) {
+      // K7s: the tile's labels, read after its MFMAs (a read at the top would wait for its LDS
+      // round trip before the first MFMA; buffer X is not rewritten before the barrier)
+      lab_v = ((const int*)(smem + LBL_OFF + X * TILE_ROWS * 4))[lane];
+      tile_mask = __ballot((uint32_t)(lab_v - lab_lo) <= lab_span);
+    }
     if (tile_mask != ~0ull) {
       mfma16_guard(acc[X]);
       const uint64_t lm = tile_mask >> (4 * g4);
@@ -702,11 +724,13 @@ __global__ __launch_bounds__(SCAN2_THREADS) void knn_scan3_kernel(ScanParams p) 
     prow = tile * TILE_ROWS + 4 * g4;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if constexpr (MODE == 0) {
+      if (may_publish) {
 #pragma unroll
-      for (int qb = 0; qb < QB; ++qb) {
-        if (theta_next[qb] != 0) theta_f[qb] = fmaxf(theta_f[qb], mrag_ord2f(theta_next[qb]));
-        thr[qb] = fmaxf(ls[qb][KL3 - 1], theta_f[qb]);
-        asm volatile("" : "+v"(theta_f[qb]), "+v"(thr[qb]));
+        for (int qb = 0; qb < QB; ++qb) {
+          if (theta_next[qb] != 0) theta_f[qb] = fmaxf(theta_f[qb], mrag_ord2f(theta_next[qb]));
+          thr[qb] = fmaxf(ls[qb][KL3 - 1], theta_f[qb]);
+          asm volatile("" : "+v"(theta_f[qb]), "+v"(thr[qb]));
+        }
       }
     }
     K7_STAMP(st2);
@@ -725,6 +749,16 @@ __global__ __launch_bounds__(SCAN2_THREADS) void knn_scan3_kernel(ScanParams p) 
 #endif
   };
 
+  if constexpr (MODE == 0) {
+    if (!may_publish) {  // the seed, read once (see the per-tile reloads in tile_body)
+#pragma unroll
+      for (int qb = 0; qb < QB; ++qb) {
+        const uint32_t t0 = __hip_atomic_load(theta_q + 16 * qb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (t0 != 0) theta_f[qb] = mrag_ord2f(t0);
+        thr[qb] = theta_f[qb];
+      }
+    }
+  }
   if (my_tiles > 0) {
 #pragma unroll
     for (int i = 0; i < GLDS_PER_WAVE; ++i) stage_piece(0, split, i, lane);
