@@ -553,7 +553,7 @@ __global__ __launch_bounds__(SCAN2_THREADS) void knn_scan3_kernel(ScanParams p) 
 #ifdef MRAG_K7_STAMPS
   // [0] tile top -> end of the DMA k-steps, [1] -> last MFMA issued, [2] -> tail + vmcnt(0),
   // [3] -> after the barrier, [4] tiles
-  unsigned long long st_sum[5] = {0, 0, 0, 0, 0}, st_mid = 0;
+  unsigned long long st_sum[7] = {0, 0, 0, 0, 0, 0, 0}, st_mid = 0;
 #endif
   auto epi_group = [&](auto g_c, auto y_c) {
     constexpr int G = decltype(g_c)::value;
@@ -577,6 +577,9 @@ __global__ __launch_bounds__(SCAN2_THREADS) void knn_scan3_kernel(ScanParams p) 
 #else
       if (__any(gm > thr[qb])) {
 #endif
+#ifdef MRAG_K7_STAMPS
+        const unsigned long long fire_t0 = __builtin_amdgcn_s_memtime();
+#endif
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const float sv = av[r];
@@ -589,7 +592,60 @@ __global__ __launch_bounds__(SCAN2_THREADS) void knn_scan3_kernel(ScanParams p) 
                                  __HIP_MEMORY_SCOPE_AGENT);
         }
         thr[qb] = fmaxf(ls[qb][KL3 - 1], theta_f[qb]);
+#ifdef MRAG_K7_STAMPS
+        st_sum[5] += 1;
+        st_sum[6] += __builtin_amdgcn_s_memtime() - fire_t0;
+#endif
       }
+    }
+  };
+
+  // A fragments: fragment n = 4 kk + rb sits in a[n % NA]. QB = 4 keeps five, so fragment
+  // n + 5 is read as soon as fragment n's MFMAs are issued: 16 MFMAs before its first use
+  // (four buffers would give 12, which LDS latency under the DMA writes can exceed)
+  constexpr int NA = QB == 4 ? 5 : 4;
+  half8 a[NA];
+  const int offA0 = offA0_init;
+  auto read_a = [&](const char* tb, int kk, int rb) {
+    a[(4 * kk + rb) % NA] =
+        *(const half8*)(tb + ((offA0 ^ ((kk & 3) << 6)) + (kk >> 2) * 256 + rb * 16 * ROW_BYTES));
+  };
+
+  uint32_t m0_keep = 0;
+#ifdef MRAG_K7_STAMPS
+  unsigned long long st_end[3] = {0, 0, 0};
+#endif
+  // End of a tile: m0 back (`wait_part` false, before the masking), then (`wait_part` true) this
+  // wave's DMA of the next tile landed, the shared threshold refreshed and the barrier: every
+  // wave's DMA landed, and the tile's buffer is free for the next tile's DMA. (Moving the wait
+  // and barrier before the last row block's MFMAs, with the next tile's first fragments read
+  // under them, measured no faster: profiles/r3_k7_tail_ab.log.)
+  auto end_of_tile = [&](bool wait_part) {
+    if (!wait_part) {
+#ifdef MRAG_K7_STAMPS
+      st_end[0] = __builtin_amdgcn_s_memtime();
+#endif
+      if constexpr (CPR == 64 && QB == 4) asm volatile("s_mov_b32 m0, %0" ::"s"(m0_keep));
+    }
+    if (wait_part) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if constexpr (MODE == 0) {
+        if (may_publish) {
+#pragma unroll
+          for (int qb = 0; qb < QB; ++qb) {
+            if (theta_next[qb] != 0) theta_f[qb] = fmaxf(theta_f[qb], mrag_ord2f(theta_next[qb]));
+            thr[qb] = fmaxf(ls[qb][KL3 - 1], theta_f[qb]);
+            asm volatile("" : "+v"(theta_f[qb]), "+v"(thr[qb]));
+          }
+        }
+      }
+#ifdef MRAG_K7_STAMPS
+      st_end[1] = __builtin_amdgcn_s_memtime();
+#endif
+      __syncthreads();
+#ifdef MRAG_K7_STAMPS
+      st_end[2] = __builtin_amdgcn_s_memtime();
+#endif
     }
   };
 
@@ -613,26 +669,16 @@ __global__ __launch_bounds__(SCAN2_THREADS) void knn_scan3_kernel(ScanParams p) 
       }
     }
     const char* tb = smem + X * TILE_BYTES;
-    int lane_t = lane, offA0 = offA0_init;
+    int lane_t = lane;
     uint32_t lane16 = lane * 16;
-    asm volatile("" : "+v"(lane_t), "+v"(offA0), "+v"(lane16));
+    asm volatile("" : "+v"(lane_t), "+v"(lane16));
     // DP = 512: m0 holds the piece's LDS address from gap 1 to the DMA in gap 2 (nothing the
     // compiler emits in this loop reads m0: ds_read_b128 / MFMA / VALU / SALU only); it is saved
     // once per tile and restored before the barrier
-    uint32_t m0_keep = 0;
     uint32_t voff = 0;
     if constexpr (CPR == 64 && QB == 4) asm volatile("s_mov_b32 %0, m0" : "=s"(m0_keep));
-    // A fragments: fragment n = 4 kk + rb sits in a[n % NA]. QB = 4 keeps five, so fragment
-    // n + 5 is read as soon as fragment n's MFMAs are issued: 16 MFMAs before its first use
-    // (four buffers would give 12, which LDS latency under the DMA writes can exceed)
-    constexpr int NA = QB == 4 ? 5 : 4;
-    half8 a[NA];
-    auto read_a = [&](int kk, int rb) {
-      a[(4 * kk + rb) % NA] =
-          *(const half8*)(tb + ((offA0 ^ ((kk & 3) << 6)) + (kk >> 2) * 256 + rb * 16 * ROW_BYTES));
-    };
 #pragma unroll
-    for (int n = 0; n < NA; ++n) read_a(n >> 2, n & 3);
+    for (int n = 0; n < NA; ++n) read_a(tb, n >> 2, n & 3);
     stage_labels(Y, ntile);
     // QB = 4: the tile's row-validity mask is built in the MFMA gaps (label read at k-step KLAB,
     // ballot one k-step later; buffer X's labels are not rewritten before the end-of-tile barrier),
@@ -654,7 +700,7 @@ __global__ __launch_bounds__(SCAN2_THREADS) void knn_scan3_kernel(ScanParams p) 
             mfma16_ab0(acc[X][rb][0], a[(4 * kk + rb) % NA], qf[kk][0]);
           else
             mfma16_ab(acc[X][rb][0], a[(4 * kk + rb) % NA], qf[kk][0]);
-          if constexpr (kk + 1 < KSTEPS) read_a(kk + 1, rb);
+          if constexpr (kk + 1 < KSTEPS) read_a(tb, kk + 1, rb);
           if constexpr (kk == 0) epi_group(std::integral_constant<int, rb>{}, std::integral_constant<int, Y>{});
           __builtin_amdgcn_sched_barrier(0);
         });
@@ -673,7 +719,7 @@ __global__ __launch_bounds__(SCAN2_THREADS) void knn_scan3_kernel(ScanParams p) 
           mfma16_ab(acc[X][rb][qb], a[n % NA], qf[kk][qb]);
         // one job per MFMA gap
         if constexpr ((j & 3) == 3) {  // after the last MFMA of fragment n: fragment n + NA
-          if constexpr (n + NA < 4 * KSTEPS) read_a((n + NA) >> 2, (n + NA) & 3);
+          if constexpr (n + NA < 4 * KSTEPS) read_a(tb, (n + NA) >> 2, (n + NA) & 3);
         } else if constexpr ((j & 3) == 1) {  // piece FRONT kk + (j >> 2): m0 + source offset
           constexpr int pc = FRONT * kk + (j >> 2);
           if constexpr (CPR == 64 && (j >> 2) < FRONT && pc < GLDS_PER_WAVE) {
@@ -701,8 +747,7 @@ __global__ __launch_bounds__(SCAN2_THREADS) void knn_scan3_kernel(ScanParams p) 
         __builtin_amdgcn_sched_barrier(0);
       });
     });
-    K7_STAMP(st1);
-    if constexpr (CPR == 64 && QB == 4) asm volatile("s_mov_b32 m0, %0" ::"s"(m0_keep));
+    end_of_tile(false);
     if constexpr (QB == 1) {
       // K7s: the tile's labels, read after its MFMAs (a read at the top would wait for its LDS
       // round trip before the first MFMA; buffer X is not rewritten before the barrier)
@@ -722,29 +767,16 @@ __global__ __launch_bounds__(SCAN2_THREADS) void knn_scan3_kernel(ScanParams p) 
         }
     }
     prow = tile * TILE_ROWS + 4 * g4;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if constexpr (MODE == 0) {
-      if (may_publish) {
-#pragma unroll
-        for (int qb = 0; qb < QB; ++qb) {
-          if (theta_next[qb] != 0) theta_f[qb] = fmaxf(theta_f[qb], mrag_ord2f(theta_next[qb]));
-          thr[qb] = fmaxf(ls[qb][KL3 - 1], theta_f[qb]);
-          asm volatile("" : "+v"(theta_f[qb]), "+v"(thr[qb]));
-        }
-      }
-    }
-    K7_STAMP(st2);
-    __syncthreads();
+    end_of_tile(true);
 #ifdef MRAG_K7_STAMPS
-    K7_STAMP(st3);
     if constexpr (QB == 4) {
       st_sum[0] += st_mid - st0;
-      st_sum[1] += st1 - st_mid;
+      st_sum[1] += st_end[0] - st_mid;
     } else {
-      st_sum[1] += st1 - st0;
+      st_sum[1] += st_end[0] - st0;
     }
-    st_sum[2] += st2 - st1;
-    st_sum[3] += st3 - st2;
+    st_sum[2] += st_end[1] - st_end[0];
+    st_sum[3] += st_end[2] - st_end[1];
     st_sum[4] += 1;
 #endif
   };
@@ -779,7 +811,7 @@ __global__ __launch_bounds__(SCAN2_THREADS) void knn_scan3_kernel(ScanParams p) 
   if constexpr (MODE == 0) {
     const int wid = blockIdx.x * SCAN2_WAVES + w;
     if (lane == 0 && wid < K7_MAXWAVES)
-      for (int i = 0; i < 5; ++i) g_k7_stamps[(size_t)wid * K7_NSTAMP + i] = st_sum[i];
+      for (int i = 0; i < 7; ++i) g_k7_stamps[(size_t)wid * K7_NSTAMP + i] = st_sum[i];
   }
 #endif
 

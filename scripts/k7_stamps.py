@@ -6,7 +6,8 @@
 
 The stamp build sums, per wave, the shader-clock spans (s_memtime) of each tile's segments:
 [0] tile top -> end of the k-steps that issue the next tile's LDS-DMA, [1] -> last MFMA issued,
-[2] the tail (masking, vmcnt(0), theta), [3] the end-of-tile barrier. Printed per segment: mean
+[2] the tail (masking, vmcnt(0), theta), [3] the end-of-tile barrier, [5] group-test fires,
+[6] cycles inside the fired insert bodies. Printed per segment: mean
 cycles per tile over the waves and the 10th / 90th percentile, next to the MFMA floor (16
 cycles per 16x16x32 MFMA, MI355X_MICROARCH.md). Runs the bench's config 3 (1M x 512, Q = 1000,
 k = 10; the 256-query instance) and Q = 1 (K7s, 64-query instance). The stamps cost cycles
@@ -53,6 +54,15 @@ def summarize(name, st, mfma_per_tile):
         out[n] = {"mean": round(col.mean(), 1), "p10": round(np.percentile(col, 10), 1),
                   "p90": round(np.percentile(col, 90), 1)}
     out["total_mean"] = round(seg.sum(1).mean(), 1)
+    # group-test fires (an insert body ran) per tile and their cycles, and the per-SIMD view
+    # (wave w of every workgroup): who waits at the barrier, who fires
+    out["fires_per_tile"] = round(float((st[live, 5] / t[live]).mean()), 3)
+    out["fire_cycles_per_tile"] = round(float((st[live, 6] / t[live]).mean()), 1)
+    w = np.nonzero(live)[0] % 4
+    out["by_wave"] = {int(i): {"barrier": round(float(seg[w == i, 3].mean()), 1),
+                               "total": round(float(seg[w == i].sum(1).mean()), 1),
+                               "fires_per_tile": round(float((st[live, 5] / t[live])[w == i].mean()), 3)}
+                      for i in range(4)}
     print(json.dumps(out), flush=True)
 
 
