@@ -575,7 +575,9 @@ __global__ __launch_bounds__(SCAN2_THREADS) void knn_scan3_kernel(ScanParams p) 
       // timing ablation only (results wrong): no group test ever fires
       if (__any(gm > thr[qb]) && p.k < 0) {
 #else
-      if (__any(gm > thr[qb])) {
+      // unlikely: the fire path is laid out away from the k-step's MFMAs, so the common case falls
+      // through (no taken branch per k-step) and the two-tile loop keeps ~10 KB of hot code
+      if (__builtin_expect(__any(gm > thr[qb]), 0)) {
 #endif
 #ifdef MRAG_K7_STAMPS
         const unsigned long long fire_t0 = __builtin_amdgcn_s_memtime();
