@@ -258,8 +258,9 @@ int ensure_workspace(mrag_encoder* e, int B, int T) {
 
 // GEMM helper: C = A[M][K] . W[N][K]^T (+bias), epilogue
 int gemm(const void* A, const void* W, const void* bias, void* C, int M, int N, int K, int ldc, int epi,
-         hipStream_t s) {
+         hipStream_t s, bool lib_ok = false) {
   GemmArgs g{};
+  g.lib_ok = lib_ok ? 1 : 0;
   g.A = (const _Float16*)A;
   g.W = (const _Float16*)W;
   g.bias = (const float*)bias;
@@ -293,10 +294,11 @@ int layernorm(const float* x, const int* gather, float* y32, _Float16* y16, cons
 int clip_layer(mrag_encoder* e, const Layer& L, int B, int T, const int32_t* mask, int causal, hipStream_t s) {
   const auto& c = e->cfg;
   const int D = c.hidden, I = c.intermediate, M = B * T;
+  const bool lib = c.image_size > 0;  // the image tower's plain GEMMs may run on hipBLASLt
   float* X = (float*)e->X.p;
   _Float16* H = (_Float16*)e->H16.p;
   if (int rc = layernorm(X, nullptr, nullptr, H, L.ln1g, L.ln1b, M, D, c.ln_eps, s)) return rc;
-  if (int rc = gemm(H, L.wqkv.p, L.bqkv.p, e->QKV.p, M, 3 * D, D, 3 * D, EPI_F16, s)) return rc;
+  if (int rc = gemm(H, L.wqkv.p, L.bqkv.p, e->QKV.p, M, 3 * D, D, 3 * D, EPI_F16, s, lib)) return rc;
   AttentionArgs a{};
   a.qkv = (const _Float16*)e->QKV.p;
   a.out = (_Float16*)e->ATT.p;
@@ -307,29 +309,32 @@ int clip_layer(mrag_encoder* e, const Layer& L, int B, int T, const int32_t* mas
   a.causal = causal;
   a.scale = 1.0f / sqrtf((float)(D / c.heads));
   if (int rc = launch_attention(a, D / c.heads, s)) return rc;
-  if (int rc = gemm(e->ATT.p, L.wo.p, L.bo.p, X, M, D, D, D, EPI_F32_RESIDUAL, s)) return rc;
+  if (int rc = gemm(e->ATT.p, L.wo.p, L.bo.p, X, M, D, D, D, EPI_F32_RESIDUAL, s, lib)) return rc;
   if (int rc = layernorm(X, nullptr, nullptr, H, L.ln2g, L.ln2b, M, D, c.ln_eps, s)) return rc;
   const int act = c.act == 0 ? EPI_F16_QUICK_GELU : EPI_F16_GELU_ERF;
   if (int rc = gemm(H, L.w1.p, L.b1.p, e->F16.p, M, I, D, I, act, s)) return rc;
-  return gemm(e->F16.p, L.w2.p, L.b2.p, X, M, D, I, D, EPI_F32_RESIDUAL, s);
+  return gemm(e->F16.p, L.w2.p, L.b2.p, X, M, D, I, D, EPI_F32_RESIDUAL, s, lib);
 }
 
 // The LAST pre-LN layer of a tower that pools one row per sequence (CLIP: the class token of
 // an image, the EOS token of a text): every row's LN1 / q|k|v / attention as in clip_layer (the
 // pooled row attends to all of them), then out-proj, LN2 and the MLP only on the B pooled rows
 // `rows`, gathered into XG (f32 residual) / AG (attention output). A GEMM row, a LayerNorm row
-// and the residual add depend only on that row (every GEMM kernel accumulates in one order
-// whatever M selects it), so the pooled rows are bit-identical to the full layer's (env
-// MRAG_ENC_FULL_LAST=1 runs the full layer: A/B check in scripts/enc_dump.py). ViT-B/32 at
+// and the residual add depend only on that row (every hand-written GEMM kernel accumulates in
+// one order whatever M selects it), so the pooled rows are bit-identical to the full layer's
+// under the hand-written kernels (mrag_gemm_set_library(0); the image tower's full-layer M >=
+// 4096 GEMMs otherwise run on hipBLASLt, another order) (env MRAG_ENC_FULL_LAST=1 runs the full
+// layer: A/B check in scripts/enc_dump.py). ViT-B/32 at
 // B = 256: the layer's out-proj / fc1 / fc2 run on 256 rows instead of 12,800.
 int clip_layer_pooled(mrag_encoder* e, const Layer& L, int B, int T, const int32_t* mask, int causal, const int* rows,
                       hipStream_t s) {
   const auto& c = e->cfg;
   const int D = c.hidden, I = c.intermediate, M = B * T;
+  const bool lib = c.image_size > 0;  // the image tower's plain GEMMs may run on hipBLASLt
   float* X = (float*)e->X.p;
   _Float16* H = (_Float16*)e->H16.p;
   if (int rc = layernorm(X, nullptr, nullptr, H, L.ln1g, L.ln1b, M, D, c.ln_eps, s)) return rc;
-  if (int rc = gemm(H, L.wqkv.p, L.bqkv.p, e->QKV.p, M, 3 * D, D, 3 * D, EPI_F16, s)) return rc;
+  if (int rc = gemm(H, L.wqkv.p, L.bqkv.p, e->QKV.p, M, 3 * D, D, 3 * D, EPI_F16, s, lib)) return rc;
   AttentionArgs a{};
   a.qkv = (const _Float16*)e->QKV.p;
   a.out = (_Float16*)e->ATT.p;
@@ -599,7 +604,7 @@ int mrag_encoder_embed_images(mrag_encoder* e, const uint8_t* images, int32_t ba
   }
   float* X = (float*)e->X.p;
   if (int rc = launch_vit_im2col(img, (_Float16*)e->F16.p, B, S, P, s)) return rc;
-  if (int rc = gemm(e->F16.p, e->patch_w.p, nullptr, e->PATCH.p, B * (T - 1), D, Kp, D, EPI_F32, s)) return rc;
+  if (int rc = gemm(e->F16.p, e->patch_w.p, nullptr, e->PATCH.p, B * (T - 1), D, Kp, D, EPI_F32, s, true)) return rc;
   if (int rc = launch_vit_embed_ln((const float*)e->PATCH.p, (const float*)e->cls.p, (const float*)e->pos.p,
                                    (const float*)e->pre_g.p, (const float*)e->pre_b.p, X, B, T, D, c.ln_eps, s))
     return rc;
@@ -776,7 +781,9 @@ int mrag_gemm_nt(const void* A, const void* W, const float* bias, void* C, int32
                  int32_t epilogue, void* stream) {
   MRAG_REQUIRE(A && W && C, "NULL pointer");
   MRAG_REQUIRE(M >= 0 && N > 0 && K > 0, "bad shape");
-  return gemm(A, W, bias, C, M, N, K, N, epilogue, (hipStream_t)stream);
+  return gemm(A, W, bias, C, M, N, K, N, epilogue, (hipStream_t)stream, /*lib_ok=*/true);
 }
+
+int mrag_gemm_set_library(int32_t mode) { return mrag_enc::set_blaslt_mode(mode); }
 
 }  // extern "C"

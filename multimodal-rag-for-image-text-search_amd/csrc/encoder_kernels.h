@@ -19,6 +19,7 @@ struct GemmArgs {
   const float* bias;  // [N] or null
   void* C;            // [M][ldc] f16 or f32 per epilogue
   int M, N, K, lda, ldw, ldc;
+  int lib_ok;         // the call may run on hipBLASLt (plain epilogues, M >= 4096: blaslt.cpp)
 };
 
 struct LayerNormArgs {
@@ -41,6 +42,10 @@ struct AttentionArgs {
 };
 
 int launch_gemm(const GemmArgs& g, int epi, hipStream_t s);
+// plain epilogues (bias, residual, f32) on hipBLASLt where selected (blaslt.cpp)
+bool blaslt_eligible(const GemmArgs& g, int epi);
+int set_blaslt_mode(int mode);
+int launch_gemm_blaslt(const GemmArgs& g, int epi, hipStream_t s);
 int launch_layernorm(const LayerNormArgs& a, hipStream_t s);
 int launch_attention(const AttentionArgs& a, int dh, hipStream_t s);
 int launch_vit_im2col(const uint8_t* img, _Float16* out, int B, int S, int P, hipStream_t s);
