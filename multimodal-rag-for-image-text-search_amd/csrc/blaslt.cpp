@@ -2,9 +2,10 @@
 // the vendor library, at the batch sizes where it is measured faster than the hand-written K3 /
 // K3d (M >= 4096 rows; notes/gemm_experiments.md), for the CLIP image tower only (GemmArgs::lib_ok):
 // the text towers keep the hand-written kernels everywhere, so a query's embedding — and with it
-// retrieve_batch == retrieve() — does not depend on its batch. The GEMMs with a fused activation
-// (quick_gelu, erf GELU: the MLP fc1) stay on K3 / K3d (the library's swish / GELU epilogues are
-// not those functions).
+// retrieve_batch == retrieve() — does not depend on its batch. The image tower's fc1 (quick_gelu)
+// runs as the library's swish: quick_gelu(z) = swish(1.702 z) / 1.702, so fc1 takes alpha = 1.702
+// and a bias pre-scaled by 1.702, and fc2 takes alpha = 1 / 1.702 (encoder.hip clip_layer); the
+// erf GELU (BERT) has no library form and stays on K3 / K3d.
 //
 // Row-major C[M][N] = A[M][K] . W[N][K]^T (+ bias[N]) (+ C for the residual) is the column-major
 // product D (N x M, ld = ldc) = op_T(W: K x N, ld = ldw) . op_N(A: K x M, ld = lda), bias along D's
@@ -53,7 +54,10 @@ bool build_plan(State& S, const GemmArgs& g, int epi, Plan& p) {
   const int32_t ta = HIPBLAS_OP_T, tb = HIPBLAS_OP_N;
   hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_TRANSA, &ta, sizeof(ta));
   hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_TRANSB, &tb, sizeof(tb));
-  if (g.bias) {
+  if (epi == EPI_F16_SWISH_LIB) {
+    const uint32_t e = g.bias ? HIPBLASLT_EPILOGUE_SWISH_BIAS_EXT : HIPBLASLT_EPILOGUE_SWISH_EXT;
+    hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_EPILOGUE, &e, sizeof(e));
+  } else if (g.bias) {
     const uint32_t e = HIPBLASLT_EPILOGUE_BIAS;
     hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_EPILOGUE, &e, sizeof(e));
   }
@@ -100,11 +104,16 @@ int set_blaslt_mode(int mode) {
   return prev;
 }
 
-bool blaslt_eligible(const GemmArgs& g, int epi) {
-  if (!g.lib_ok || (epi != EPI_F16 && epi != EPI_F32_RESIDUAL && epi != EPI_F32)) return false;
+bool blaslt_takes(int M) {
   // large-M calls only: small batches keep the hand-written kernels, and with them a row's result
   // independent of its batch size there
-  return blaslt_mode() != 0 && g.M >= 4096;
+  return blaslt_mode() != 0 && M >= 4096;
+}
+
+bool blaslt_eligible(const GemmArgs& g, int epi) {
+  if (!g.lib_ok || (epi != EPI_F16 && epi != EPI_F32_RESIDUAL && epi != EPI_F32 && epi != EPI_F16_SWISH_LIB))
+    return false;
+  return blaslt_takes(g.M);
 }
 
 // MRAG_OK, or MRAG_ERR_UNSUPPORTED when the library has no algorithm for the shape (the caller
@@ -141,7 +150,8 @@ int launch_gemm_blaslt(const GemmArgs& g, int epi, hipStream_t s) {
   // the bias pointer is per call (a shape's plan serves every layer): set it on a private copy
   // of the descriptor would need one descriptor per call; instead the plan is keyed per bias
   // presence and the pointer is set under the lock right before the launch
-  const float alpha = 1.f, beta = epi == EPI_F32_RESIDUAL ? 1.f : 0.f;
+  // D = act(alpha (W A) + beta C + bias): the bias is not scaled by alpha
+  const float alpha = g.alpha != 0.f ? g.alpha : 1.f, beta = epi == EPI_F32_RESIDUAL ? 1.f : 0.f;
   std::lock_guard<std::mutex> lk(S.mu);
   if (g.bias)
     hipblasLtMatmulDescSetAttribute(plan->desc, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &g.bias, sizeof(g.bias));

@@ -46,7 +46,9 @@ void buf_free(Buf& b) {
 
 struct Layer {
   Buf wqkv, bqkv, wo, bo, w1, b1, w2, b2, ln1g, ln1b, ln2g, ln2b;
+  Buf b1s;  // image tower: QUICK_GELU_SLOPE * b1 (fc1 as the library's swish, clip_layer)
 };
+constexpr float QUICK_GELU_SLOPE = 1.702f;  // quick_gelu(z) = z sigmoid(1.702 z) = swish(1.702 z) / 1.702
 
 __global__ void f32_to_f16_kernel(const float* __restrict__ in, _Float16* __restrict__ out, int64_t n) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -258,9 +260,10 @@ int ensure_workspace(mrag_encoder* e, int B, int T) {
 
 // GEMM helper: C = A[M][K] . W[N][K]^T (+bias), epilogue
 int gemm(const void* A, const void* W, const void* bias, void* C, int M, int N, int K, int ldc, int epi,
-         hipStream_t s, bool lib_ok = false) {
+         hipStream_t s, bool lib_ok = false, float alpha = 0.f) {
   GemmArgs g{};
   g.lib_ok = lib_ok ? 1 : 0;
+  g.alpha = alpha;
   g.A = (const _Float16*)A;
   g.W = (const _Float16*)W;
   g.bias = (const float*)bias;
@@ -312,6 +315,17 @@ int clip_layer(mrag_encoder* e, const Layer& L, int B, int T, const int32_t* mas
   if (int rc = gemm(e->ATT.p, L.wo.p, L.bo.p, X, M, D, D, D, EPI_F32_RESIDUAL, s, lib)) return rc;
   if (int rc = layernorm(X, nullptr, nullptr, H, L.ln2g, L.ln2b, M, D, c.ln_eps, s)) return rc;
   const int act = c.act == 0 ? EPI_F16_QUICK_GELU : EPI_F16_GELU_ERF;
+  if (lib && c.act == 0 && L.b1s.p && blaslt_takes(M)) {
+    // the MLP on the library: F16 = swish(1.702 (H W1^T + b1)) = 1.702 quick_gelu(...), then
+    // X += (1 / 1.702) F16 W2^T + b2 (the bias is not scaled by alpha)
+    int rc = gemm(H, L.w1.p, L.b1s.p, e->F16.p, M, I, D, I, EPI_F16_SWISH_LIB, s, true, QUICK_GELU_SLOPE);
+    if (rc == MRAG_OK) {
+      rc = gemm(e->F16.p, L.w2.p, L.b2.p, X, M, D, I, D, EPI_F32_RESIDUAL, s, true, 1.0f / QUICK_GELU_SLOPE);
+      if (rc != MRAG_ERR_UNSUPPORTED) return rc;  // else: fc1 again by hand below, fc2 with it
+    } else if (rc != MRAG_ERR_UNSUPPORTED) {
+      return rc;
+    }
+  }
   if (int rc = gemm(H, L.w1.p, L.b1.p, e->F16.p, M, I, D, I, act, s)) return rc;
   return gemm(e->F16.p, L.w2.p, L.b2.p, X, M, D, I, D, EPI_F32_RESIDUAL, s, lib);
 }
@@ -449,7 +463,8 @@ int mrag_encoder_destroy(mrag_encoder* e) {
     if (e->done) (void)hipEventDestroy(e->done);
     if (e->null_ev) (void)hipEventDestroy(e->null_ev);
     for (auto& L : e->layers)
-      for (Buf* b : {&L.wqkv, &L.bqkv, &L.wo, &L.bo, &L.w1, &L.b1, &L.w2, &L.b2, &L.ln1g, &L.ln1b, &L.ln2g, &L.ln2b})
+      for (Buf* b : {&L.wqkv, &L.bqkv, &L.wo, &L.bo, &L.w1, &L.b1, &L.w2, &L.b2, &L.ln1g, &L.ln1b, &L.ln2g, &L.ln2b,
+                     &L.b1s})
         buf_free(*b);
     for (Buf* b : {&e->patch_w, &e->cls, &e->pos, &e->pre_g, &e->pre_b, &e->post_g, &e->post_b, &e->proj_w, &e->tok,
                    &e->type0, &e->emb_g, &e->emb_b, &e->X, &e->H16, &e->QKV, &e->ATT, &e->F16, &e->PATCH, &e->IMG,
@@ -499,6 +514,12 @@ int mrag_encoder_set_param(mrag_encoder* e, const char* cname, const float* data
       rc = is_w ? upload(L.wo, data, numel, true, s) : upload(L.bo, data, numel, false, s);
     } else if (name.find("fc1") != std::string::npos || name.find("intermediate.dense") != std::string::npos) {
       rc = is_w ? upload(L.w1, data, numel, true, s) : upload(L.b1, data, numel, false, s);
+      if (rc == MRAG_OK && !is_w && c.image_size > 0 && c.act == 0) {  // image tower: the swish-form bias
+        std::vector<float> sc((size_t)numel);
+        for (int64_t i = 0; i < numel; ++i) sc[(size_t)i] = QUICK_GELU_SLOPE * data[i];
+        rc = upload(L.b1s, sc.data(), numel, false, s);
+        if (rc == MRAG_OK) MRAG_HIP(hipStreamSynchronize(s));  // sc is a host temporary
+      }
     } else if (name.find("fc2") != std::string::npos || name.find("output.dense") != std::string::npos) {
       rc = is_w ? upload(L.w2, data, numel, true, s) : upload(L.b2, data, numel, false, s);
     } else if (name.find("layer_norm1") != std::string::npos ||

@@ -11,6 +11,7 @@ enum Epilogue {
   EPI_F16_GELU_ERF = 2,    // C16 = gelu_erf(acc + bias)         (BERT intermediate)
   EPI_F32_RESIDUAL = 3,    // C32 += acc + bias                  (out-proj / fc2 into the residual)
   EPI_F32 = 4,             // C32 = acc + bias                   (patch embed, projections)
+  EPI_F16_SWISH_LIB = 5,   // C16 = swish(alpha acc + bias), hipBLASLt only (image-tower fc1, blaslt.cpp)
 };
 
 struct GemmArgs {
@@ -20,6 +21,7 @@ struct GemmArgs {
   void* C;            // [M][ldc] f16 or f32 per epilogue
   int M, N, K, lda, ldw, ldc;
   int lib_ok;         // the call may run on hipBLASLt (plain epilogues, M >= 4096: blaslt.cpp)
+  float alpha;        // C = alpha acc (+ ...): hipBLASLt only; 0 or 1 = none (K3 / K3d have none)
 };
 
 struct LayerNormArgs {
@@ -44,6 +46,7 @@ struct AttentionArgs {
 int launch_gemm(const GemmArgs& g, int epi, hipStream_t s);
 // plain epilogues (bias, residual, f32) on hipBLASLt where selected (blaslt.cpp)
 bool blaslt_eligible(const GemmArgs& g, int epi);
+bool blaslt_takes(int M);  // the library is selected and M is large enough (image tower)
 int set_blaslt_mode(int mode);
 int launch_gemm_blaslt(const GemmArgs& g, int epi, hipStream_t s);
 int launch_layernorm(const LayerNormArgs& a, hipStream_t s);

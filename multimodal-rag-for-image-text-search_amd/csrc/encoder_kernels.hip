@@ -1083,9 +1083,12 @@ int launch_gemm(const GemmArgs& g, int epi, hipStream_t s) {
   MRAG_REQUIRE(g.N % GN == 0 && g.K % GK == 0, "gemm: N=%d must be a multiple of %d and K=%d of %d", g.N, GN, g.K,
                GK);
   MRAG_REQUIRE(g.lda % 8 == 0 && g.ldw % 8 == 0 && g.ldc % 4 == 0, "gemm: lda/ldw must be multiples of 8, ldc of 4");
+  const bool lib_only = epi == EPI_F16_SWISH_LIB || (g.alpha != 0.f && g.alpha != 1.f);
   if (blaslt_eligible(g, epi)) {
     const int rc = launch_gemm_blaslt(g, epi, s);
-    if (rc != MRAG_ERR_UNSUPPORTED) return rc;
+    if (rc != MRAG_ERR_UNSUPPORTED || lib_only) return rc;
+  } else if (lib_only) {
+    return MRAG_ERR_UNSUPPORTED;  // no hand-written form: the caller takes its K3 / K3d path
   }
   if (g.M >= 1024 && g.N <= G8_BIAS_MAX && g.N % 256 == 0 && !k3_beats_k3d(g)) {
     const int ntiles = ((g.M + G8Geom::BM - 1) / G8Geom::BM) * (g.N / G8Geom::BN);
