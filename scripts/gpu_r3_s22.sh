@@ -1,0 +1,16 @@
+#!/bin/bash
+# Round 3, session 22: K7 next-tile DMA pieces issued inside one asm with their m0 write and an MFMA
+# (no compiler s_nop per piece) A/B vs HEAD (libmrag_base.so); stamps; kNN tests.
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd $R; mkdir -p gpurun_out
+L=multimodal-rag-for-image-text-search_amd/lib
+timeout -k 10 900 python -u -m pytest tests/test_knn_gpu.py tests/test_knn_generic_gpu.py -x -q -m gpu --timeout 600 --timeout-method thread > gpurun_out/r3s22_tests.log 2>&1 || { echo "pytest failed"; tail -30 gpurun_out/r3s22_tests.log; exit 1; }
+tail -1 gpurun_out/r3s22_tests.log
+for round in 1 2 3; do
+  for lib in libmrag_base.so libmrag.so; do
+    MRAG_LIB=$L/$lib timeout -k 10 120 python scripts/knn_scan_ab.py 30 >> gpurun_out/r3s22_ab.log 2>&1 || { echo "ab $lib failed"; tail -5 gpurun_out/r3s22_ab.log; exit 2; }
+  done
+done
+grep -v amdgpu.ids gpurun_out/r3s22_ab.log
+MRAG_LIB=$L/libmrag_k7stamp.so timeout -k 10 120 python scripts/k7_stamps.py >> gpurun_out/r3s22_stamps.log 2>&1 || { echo "stamps failed"; tail -5 gpurun_out/r3s22_stamps.log; exit 3; }
+grep -v amdgpu.ids gpurun_out/r3s22_stamps.log | grep QB4 | cut -c1-600
