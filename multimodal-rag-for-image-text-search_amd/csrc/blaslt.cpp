@@ -11,7 +11,7 @@
 // product D (N x M, ld = ldc) = op_T(W: K x N, ld = ldw) . op_N(A: K x M, ld = lda), bias along D's
 // rows. One plan (descriptors + the heuristic's first algorithm) per shape and epilogue, built
 // once under a lock; one workspace per HIP stream (a stream-K algorithm keeps partial tiles
-// there, so two streams never share one).
+// there, so two streams never share one), sized to the largest plan that stream has run.
 #include <hipblaslt/hipblaslt.h>
 
 #include <atomic>
@@ -40,7 +40,11 @@ struct State {
   bool init = false, usable = false;
   hipblasLtHandle_t h = nullptr;
   std::map<std::tuple<int, int, int, int, int, int, int, bool>, Plan> plans;
-  std::map<hipStream_t, void*> ws;
+  struct Ws {
+    void* p = nullptr;
+    size_t bytes = 0;
+  };
+  std::map<hipStream_t, Ws> ws;
 };
 State& st() {
   static State s;
@@ -139,12 +143,21 @@ int launch_gemm_blaslt(const GemmArgs& g, int epi, hipStream_t s) {
     if (!it->second.ok) return MRAG_ERR_UNSUPPORTED;
     plan = &it->second;
     if (plan->ws > 0) {
-      void*& w = S.ws[s];
-      if (!w && hipMalloc(&w, WS_BYTES) != hipSuccess) {
-        w = nullptr;
-        return MRAG_ERR_UNSUPPORTED;
+      State::Ws& w = S.ws[s];
+      if (w.bytes < plan->ws) {  // grow: the stream's earlier calls may still be reading the old one
+        if (w.p) {
+          (void)hipStreamSynchronize(s);
+          (void)hipFree(w.p);
+          w.p = nullptr;
+          w.bytes = 0;
+        }
+        if (hipMalloc(&w.p, plan->ws) != hipSuccess) {
+          w.p = nullptr;
+          return MRAG_ERR_UNSUPPORTED;
+        }
+        w.bytes = plan->ws;
       }
-      ws = w;
+      ws = w.p;
     }
   }
   // the bias pointer is per call (a shape's plan serves every layer): set it on a private copy
