@@ -895,6 +895,128 @@ __global__ __launch_bounds__(256) void attention_flash16_kernel(AttentionArgs a)
 // in f32 (app/ml/embeddings.py:85; bit-exact formula verified in SURVEY.md §8a a2), then the
 // Conv2d(3, 768, k=32, s=32) as a GEMM with K ordered (c, kh, kw) like the torch weight.
 // img: [B][S][S][3] u8 (HWC, the decoded RGB image), out: [B*G*G][3*P*P] f16.
+// K4 v3, one sequence per workgroup (33 <= L <= 64: the ViT's 50 tokens): the four waves are the
+// sequence's (up to) four 16-query blocks of one head, and the head's K and V rows are staged into
+// LDS ONCE by all 256 threads (one round trip) instead of each wave loading every key block in
+// turn (four dependent global round trips per wave: 27.8 us per ViT layer, latency-bound). The
+// per-wave arithmetic is attention_flash16_kernel's, operand for operand (K fragments and the
+// transposed V reads come from the shared image), so the outputs are bit-identical to it.
+template <int DH>
+__global__ __launch_bounds__(256) void attention_seq64_kernel(AttentionArgs a) {
+  constexpr int KS = DH / 32, DB = DH / 16;
+  constexpr int VROW = DH == 64 ? 96 : 48;  // as attention_flash16_kernel
+  constexpr int KROW = DH + 8;              // K image row stride (halves): 16-B reads of 16 rows spread banks
+  typedef _Float16 half4_v __attribute__((ext_vector_type(4)));
+  __shared__ __attribute__((aligned(16))) _Float16 Ks[64 * KROW];
+  __shared__ __attribute__((aligned(16))) _Float16 Vs[64 * VROW];
+  __shared__ int kok[64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = lane & 15, g = lane >> 4;
+  const int L = a.L, nqb = (L + 15) >> 4;
+  const int bh = blockIdx.x, hd = bh % a.H, b = bh / a.H;
+  const int D = a.H * DH;
+  const size_t rs = (size_t)3 * D;
+  const _Float16* base = a.qkv + (size_t)b * L * rs + hd * DH;
+  // stage: 64 key rows x DH of K and of V (zeros past L), 16 B per thread per step; every global
+  // load (K, V, the mask flag, this wave's Q fragments) is issued before the first LDS store, so
+  // a workgroup pays one memory round trip
+  constexpr int CH = DH / 8;             // 16-byte chunks per row
+  constexpr int NST = 64 * CH / 256;     // staging steps per thread
+  static_assert(NST * 256 == 64 * CH, "64 rows of DH halves in whole 256-thread steps");
+  half8 kv[NST], vv[NST];
+  // (rows past L load row L - 1, unconditionally, and are zeroed at the store: a conditional load
+  // made the compiler wait for it at the branch join)
+#pragma unroll
+  for (int t = 0; t < NST; ++t) {
+    const int idx = threadIdx.x + 256 * t, key = min(idx / CH, L - 1), ch = idx % CH;
+    kv[t] = *(const half8*)(base + (size_t)key * rs + D + 8 * ch);
+    vv[t] = *(const half8*)(base + (size_t)key * rs + 2 * D + 8 * ch);
+  }
+  const int qb = w;
+  const int qrow = 16 * qb + c;
+  half8 qf[KS];
+#pragma unroll
+  for (int st = 0; st < KS; ++st) qf[st] = *(const half8*)(base + (size_t)min(qrow, L - 1) * rs + 32 * st + 8 * g);
+  int ok = 0;
+  if (threadIdx.x < 64) {
+    const int key = threadIdx.x;
+    ok = key < L && (!a.mask || a.mask[(size_t)b * L + key] != 0);
+  }
+#pragma unroll
+  for (int t = 0; t < NST; ++t) {
+    const int idx = threadIdx.x + 256 * t, key = idx / CH, ch = idx % CH;
+    *(half8*)(Ks + key * KROW + 8 * ch) = key < L ? kv[t] : half8{};
+    *(half8*)(Vs + key * VROW + 8 * ch) = key < L ? vv[t] : half8{};
+  }
+  if (threadIdx.x < 64) kok[threadIdx.x] = ok;
+  if (qrow >= L) {
+#pragma unroll
+    for (int st = 0; st < KS; ++st) qf[st] = half8{};
+  }
+  __syncthreads();
+  if (qb >= nqb) return;  // whole wave, after the barrier
+  f32x4 o[DB];
+#pragma unroll
+  for (int db = 0; db < DB; ++db) o[db] = f32x4{};
+  float m = -INFINITY, l = 0.f;
+  const int nkb = a.causal ? min(nqb, qb + 1) : nqb;
+  for (int kb = 0; kb < nkb; ++kb) {
+    bool kv[4], any_ok = false;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int key = 16 * kb + 4 * g + r;
+      kv[r] = kok[key] != 0 && (!a.causal || key <= qrow);
+      any_ok |= kv[r];
+    }
+    if (!__any(any_ok)) continue;  // wave-uniform: a fully masked key block
+    f32x4 sacc = {};
+#pragma unroll
+    for (int st = 0; st < KS; ++st) {
+      const half8 kf = *(const half8*)(Ks + (16 * kb + c) * KROW + 32 * st + 8 * g);
+      sacc = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf, qf[st], sacc, 0, 0, 0);
+    }
+    float sv[4], bmax = -INFINITY;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      sv[r] = kv[r] ? sacc[r] * a.scale : -INFINITY;
+      bmax = fmaxf(bmax, sv[r]);
+    }
+    bmax = fmaxf(bmax, __shfl_xor(bmax, 16));
+    bmax = fmaxf(bmax, __shfl_xor(bmax, 32));
+    const float mn = fmaxf(m, bmax);
+    const float alpha = m == -INFINITY ? 0.f : __expf(m - mn);
+    half4_v pf;
+    float ps = 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float pv = sv[r] == -INFINITY ? 0.f : __expf(sv[r] - mn);
+      pf[r] = (_Float16)pv;
+      ps += pv;
+    }
+    ps += __shfl_xor(ps, 16);
+    ps += __shfl_xor(ps, 32);
+    l = l * alpha + ps;
+    m = mn;
+    const _Float16* vs = Vs + 16 * kb * VROW;
+#pragma unroll
+    for (int db = 0; db < DB; ++db) {
+      o[db] *= alpha;
+      const half4_t vt = lds_read_tr16(vs + (4 * g + (c >> 2)) * VROW + 16 * db + 4 * (c & 3));
+      o[db] = __builtin_amdgcn_mfma_f32_16x16x16f16(vt, pf, o[db], 0, 0, 0);
+    }
+  }
+  if (qrow < L) {
+    const float inv = l > 0.f ? 1.f / l : 0.f;
+    _Float16* orow = a.out + ((size_t)b * L + qrow) * D + hd * DH + 4 * g;
+#pragma unroll
+    for (int db = 0; db < DB; ++db) {
+      const half4_t h = {(_Float16)(o[db][0] * inv), (_Float16)(o[db][1] * inv), (_Float16)(o[db][2] * inv),
+                         (_Float16)(o[db][3] * inv)};
+      *(half4_t*)(orow + 16 * db) = h;
+    }
+  }
+}
+
 __global__ void vit_im2col_kernel(const uint8_t* __restrict__ img, _Float16* __restrict__ out, int B, int S,
                                   int P) {
   const int G = S / P;
@@ -1133,8 +1255,17 @@ int launch_attention(const AttentionArgs& a, int dh, hipStream_t s) {
   MRAG_REQUIRE(dh == 64 || dh == 32, "attention: head_dim %d unsupported (32, 64)", dh);
   const int64_t items = (int64_t)a.B * a.H * ((a.L + 15) / 16);
   MRAG_REQUIRE(items < (1ll << 33), "attention: batch too large");
-  hipLaunchKernelGGL(dh == 64 ? attention_flash16_kernel<64> : attention_flash16_kernel<32>,
-                     dim3((unsigned)((items + 3) / 4)), dim3(256), 0, s, a);
+  static const bool seq64 = [] {
+    const char* e = getenv("MRAG_ATTN_SEQ64");
+    return !(e && atoi(e) == 0);
+  }();
+  if (seq64 && a.L > 32 && a.L <= 64) {  // one workgroup per (sequence, head): the ViT's 50 tokens
+    hipLaunchKernelGGL(dh == 64 ? attention_seq64_kernel<64> : attention_seq64_kernel<32>,
+                       dim3((unsigned)((int64_t)a.B * a.H)), dim3(256), 0, s, a);
+  } else {
+    hipLaunchKernelGGL(dh == 64 ? attention_flash16_kernel<64> : attention_flash16_kernel<32>,
+                       dim3((unsigned)((items + 3) / 4)), dim3(256), 0, s, a);
+  }
   MRAG_CHECK_LAUNCH();
   return MRAG_OK;
 }
