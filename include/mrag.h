@@ -223,7 +223,8 @@ int mrag_image_resize_crop(const uint8_t* pixels, const int64_t* offsets, const 
 
 /* K3 building block: C[M][N] (op)= A[M][K] . W[N][K]^T + bias (device pointers;
  * A, W fp16 row-major; epilogue 0 f16 out, 1 f16 quick_gelu, 2 f16 gelu_erf,
- * 3 f32 C += , 4 f32 out). N % 128 == 0, K % 64 == 0. */
+ * 3 f32 C += , 4 f32 out, 5 f16 swish = x sigmoid(x): the library only, M >= 4096, else
+ * MRAG_ERR_UNSUPPORTED). N % 128 == 0, K % 64 == 0. */
 int mrag_gemm_nt(const void* A, const void* W, const float* bias, void* C, int32_t M, int32_t N, int32_t K,
                  int32_t epilogue, void* stream);
 
