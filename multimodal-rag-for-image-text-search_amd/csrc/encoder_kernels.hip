@@ -700,6 +700,11 @@ __global__ __launch_bounds__(256) void layernorm4_kernel(LayerNormArgs a) {
 // wave left every wave waiting on its own loads: ViT LayerNorm 13.6 -> 11.7 us; 2 and 8
 // workgroups per CU measured 13.4 / 12.6 us).
 constexpr int LN_WG_PER_CU = 4;
+// Every load is unconditional (the prefetch of the last row re-loads it; chunks past the row load
+// the row's last chunk and are zeroed after the wait) and the gather form is its own instance:
+// with conditional loads the compiler merged the branch joins' counters and waited for ALL loads
+// (`vmcnt(0)`, the prefetch included) before each row's reductions, so nothing overlapped.
+template <bool GATHER>
 __global__ __launch_bounds__(256) void layernorm_stream_kernel(LayerNormArgs a) {
   const int lane = threadIdx.x & 63;
   const int nw = (int)gridDim.x * 4;
@@ -709,16 +714,18 @@ __global__ __launch_bounds__(256) void layernorm_stream_kernel(LayerNormArgs a) 
   f32x4 g4[4], b4[4];
   ln_params4(lane, a.D, a.gamma, a.beta, g4, b4);
   auto load = [&](int row, f32x4(&v)[4]) {
-    const int src = a.gather ? a.gather[row] : row;
+    const int src = GATHER ? a.gather[row] : row;
     const f32x4* x = (const f32x4*)(a.x + (size_t)src * a.ldx);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) v[j] = lane + 64 * j < nc ? x[lane + 64 * j] : f32x4{};
+    for (int j = 0; j < 4; ++j) v[j] = x[min(lane + 64 * j, nc - 1)];
   };
   f32x4 v[4], vn[4];
   load(r, v);
   for (; r < a.rows; r += nw) {
-    const int rn = r + nw;
-    if (rn < a.rows) load(rn, vn);
+    load(min(r + nw, a.rows - 1), vn);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (lane + 64 * j >= nc) v[j] = f32x4{};  // ln_row4p: v = 0 past the row
     ln_row4p(v, lane, a.D, a.eps, g4, b4, a.y32 ? a.y32 + (size_t)r * a.D : nullptr,
              a.y16 ? a.y16 + (size_t)r * a.D : nullptr);
 #pragma unroll
@@ -1230,7 +1237,10 @@ int launch_layernorm(const LayerNormArgs& a, hipStream_t s) {
   const bool alias = a.gather && a.y32 == a.x;
   if (vec4 && !alias) {
     const int nb = std::min((a.rows + 3) / 4, num_cus() * LN_WG_PER_CU);
-    hipLaunchKernelGGL(layernorm_stream_kernel, dim3((unsigned)nb), dim3(256), 0, s, a);
+    if (a.gather)
+      hipLaunchKernelGGL(layernorm_stream_kernel<true>, dim3((unsigned)nb), dim3(256), 0, s, a);
+    else
+      hipLaunchKernelGGL(layernorm_stream_kernel<false>, dim3((unsigned)nb), dim3(256), 0, s, a);
   } else if (vec4)
     hipLaunchKernelGGL(layernorm4_kernel, dim3((unsigned)((a.rows + 3) / 4)), dim3(256), 0, s, a);
   else
