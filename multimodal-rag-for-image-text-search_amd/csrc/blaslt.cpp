@@ -46,9 +46,15 @@ struct State {
   };
   std::map<hipStream_t, Ws> ws;
 };
+// one state per device: a hipBLASLt handle (and the algorithms it picks) belongs to the device
+// that was current when it was created, and a process may drive several
 State& st() {
-  static State s;
-  return s;
+  static std::mutex mu;
+  static std::map<int, State> per_dev;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  std::lock_guard<std::mutex> lk(mu);
+  return per_dev[dev];  // std::map nodes are stable
 }
 
 bool build_plan(State& S, const GemmArgs& g, int epi, Plan& p) {
@@ -160,9 +166,8 @@ int launch_gemm_blaslt(const GemmArgs& g, int epi, hipStream_t s) {
       ws = w.p;
     }
   }
-  // the bias pointer is per call (a shape's plan serves every layer): set it on a private copy
-  // of the descriptor would need one descriptor per call; instead the plan is keyed per bias
-  // presence and the pointer is set under the lock right before the launch
+  // the bias pointer is per call (a shape's plan serves every layer), so it is set on the shared
+  // descriptor under the lock, right before the launch that reads it
   // D = act(alpha (W A) + beta C + bias): the bias is not scaled by alpha
   const float alpha = g.alpha != 0.f ? g.alpha : 1.f, beta = epi == EPI_F32_RESIDUAL ? 1.f : 0.f;
   std::lock_guard<std::mutex> lk(S.mu);
