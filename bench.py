@@ -562,6 +562,9 @@ def fusion_leg(world: int, rank: int, local: int, steps: int, warmup: int):
         "one_step_in_flight": None if one_dt is None else {"queries_per_s": round(NQ * steps / one_dt, 1),
                                                           "ms_per_step": round(one_dt / steps * 1e3, 3)},
         "fused_hits_last_step": int((pick >= 0).sum()),
+        # queries whose fp16 top-k the certificate could not prove in the last search of each index
+        # (they take the exact collect pass: correct, one more scan of their query group)
+        "uncertified_last_search": {"text": text_sh.local.last_stats()[0], "image": img_sh.local.last_stats()[0]},
         "roofline": {"bound": "mfma", "scope": "whole step (towers + both scans; fusion and copies add no FLOP)",
                      "achieved": round(achieved, 2), "peak": MFMA_FP16_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(achieved / MFMA_FP16_PEAK_TFLOPS, 4),
