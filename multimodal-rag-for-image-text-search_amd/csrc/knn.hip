@@ -1507,6 +1507,19 @@ int scan3_qb(int64_t nq) {
   return nq <= small_max ? 1 : 4;
 }
 
+// Sample pre-pass stride for k: the main scan's fires grow with the rows above the seed, about
+// k x stride, so k > 16 samples every 4th tile (512k x 512, k = 50: search 0.824 -> 0.736 ms,
+// scan 0.659 -> 0.501; stride 8: 0.748; notes/knn_scan_experiments.md). Env
+// MRAG_K7_STRIDE_BIGK (experiment) sets the k > 16 stride.
+int sample_stride_for(int k) {
+  static const int big = [] {
+    const char* e = getenv("MRAG_K7_STRIDE_BIGK");
+    const int v = e ? atoi(e) : 4;
+    return v >= 2 && v <= 64 ? v : 4;
+  }();
+  return k > 16 ? big : SAMPLE_STRIDE;
+}
+
 scan_fn get_scan(int DP, int KL, bool collect) {
   switch (DP) {
     case 128: return pick_scan<128>(KL, collect);
@@ -1963,9 +1976,10 @@ int mrag_knn_search(mrag_knn_index* ix, const float* queries, int64_t nq, int32_
     // (qb == 1) streams at the HBM rate, where the pre-pass costs more than the inserts it saves
     // (Q = 1: 0.270 -> 0.247 ms without it, notes/knn_scan_experiments.md).
     const int min_tiles = ntiles / S;
-    if (use_v3 && qb == 4 && min_tiles >= 4 * SAMPLE_STRIDE) {
-      sp.sample_stride = SAMPLE_STRIDE;
-      sp.sample_tiles = min_tiles / SAMPLE_STRIDE;
+    const int stride = sample_stride_for(k);
+    if (use_v3 && qb == 4 && min_tiles >= 4 * stride) {
+      sp.sample_stride = stride;
+      sp.sample_tiles = min_tiles / stride;
       hipLaunchKernelGGL(get_scan3(DP, true, qb), sgrid, dim3(SCAN2_THREADS), 0, s, sp);
       MRAG_CHECK_LAUNCH();
       hipLaunchKernelGGL(theta_init_kernel, dim3((unsigned)nq), dim3(64), 0, s, (const float*)sp.part_s, 4 * S,
@@ -2013,7 +2027,22 @@ int mrag_knn_search(mrag_knn_index* ix, const float* queries, int64_t nq, int32_
     hipLaunchKernelGGL(merge, dim3((unsigned)nq), dim3(MERGE_THREADS), msh, s, mp);
     MRAG_CHECK_LAUNCH();
 
-    {
+    // The failure count, read back right after K8: the common search certifies every query and
+    // launches nothing more; otherwise K7c's grid is sized to the failing queries alone, with
+    // more splits than the main scan (one failing query over the main scan's 64 splits is one
+    // 8-wave workgroup per split, latency-bound on its own LDS-DMA round trips: 0.3 ms over
+    // 512k rows, notes/knn_scan_experiments.md)
+    MRAG_HIP(hipMemcpyAsync(c->host_counters, c->counters.p, 8, hipMemcpyDeviceToHost, s));
+    if (int rc = wait_stream(c, s)) return rc;
+    if (profile) {
+      float ms = 0.f;
+      MRAG_HIP(hipEventElapsedTime(&ms, c->ev0, c->ev1));
+      std::lock_guard<std::mutex> lk(ix->pool_mu);
+      ix->scan_ms += ms;
+      ix->scan_launches++;
+    }
+    uncertified = c->host_counters[0];
+    if (uncertified > 0) {
       // per-slot collect capacity of this search (K7c/K10 for the uncertified queries): at
       // most 4096 rows and 64M slots in all; a query that collects more (a run of more than
       // ccap near-duplicates within eps of its k-th score) sends the batch to K7g below,
@@ -2023,7 +2052,14 @@ int mrag_knn_search(mrag_knn_index* ix, const float* queries, int64_t nq, int32_
       if (int rc = ensure(c->scratch, (size_t)Qp * ccap * 8)) return rc;
       sp.cand = (int32_t*)c->cand.p;
       sp.ccap = ccap;
-      hipLaunchKernelGGL(collect, sgrid, dim3(SCAN_THREADS), 0, s, sp);
+      // K7c: QPG failing queries per workgroup, about 1024 workgroups in all
+      const int cgroups = (int)((uncertified + QPG - 1) / QPG);
+      int Sc = std::max(S, 1024 / cgroups);
+      Sc = std::min(Sc, ntiles);
+      if (Sc >= 8) Sc &= ~7;
+      sp.qgroups = cgroups;
+      sp.splits = Sc;
+      hipLaunchKernelGGL(collect, dim3((unsigned)(cgroups * Sc)), dim3(SCAN_THREADS), 0, s, sp);
       MRAG_CHECK_LAUNCH();
       FinalParams fp{};
       fp.fail_list = sp.fail_list;
@@ -2044,18 +2080,10 @@ int mrag_knn_search(mrag_knn_index* ix, const float* queries, int64_t nq, int32_
       fp.out_r = orr;
       fp.row_offset = row_offset;
       fp.overflow = (int32_t*)c->counters.p + 1;
-      hipLaunchKernelGGL(knn_final_kernel, dim3((unsigned)nq), dim3(MERGE_THREADS), (size_t)DP * 4, s, fp);
+      hipLaunchKernelGGL(knn_final_kernel, dim3((unsigned)uncertified), dim3(MERGE_THREADS), (size_t)DP * 4, s, fp);
       MRAG_CHECK_LAUNCH();
       MRAG_HIP(hipMemcpyAsync(c->host_counters, c->counters.p, 8, hipMemcpyDeviceToHost, s));
       if (int rc = wait_stream(c, s)) return rc;
-      uncertified = c->host_counters[0];
-      if (profile) {
-        float ms = 0.f;
-        MRAG_HIP(hipEventElapsedTime(&ms, c->ev0, c->ev1));
-        std::lock_guard<std::mutex> lk(ix->pool_mu);
-        ix->scan_ms += ms;
-        ix->scan_launches++;
-      }
       if (c->host_counters[1] != 0) {
         retries = 1;
         if (int rc = mrag_knn::search_generic(generic_args(), c->gws, s, nullptr)) return rc;

@@ -21,16 +21,21 @@ for dim in (384, 512):
     ix.add(x)
     del x
     q = torch.randn((1000, dim), generator=torch.Generator(device=dev).manual_seed(1), device=dev)
-    for k in (1, 6, 10, 12, 16, 32, 50, 64):
+    for k in [int(v) for v in os.environ.get("KS", "1,6,10,12,16,32,50,64").split(",")]:
         s = torch.cuda.Stream(device=dev)
         with torch.cuda.stream(s):
             for _ in range(3):
                 ix.search(q, k)
             s.synchronize()
             ix.profile(1)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s)
             for _ in range(10):
                 ix.search(q, k)
+            e1.record(s)
             s.synchronize()
             ms, n = ix.profile(0)
             unc, _ = ix.last_stats()
-        print(json.dumps({"dim": dim, "rows": 1 << 19, "k": k, "scan_ms": round(ms / n, 4), "uncertified": unc}), flush=True)
+        print(json.dumps({"dim": dim, "rows": 1 << 19, "k": k, "scan_ms": round(ms / n, 4),
+                          "search_ms": round(e0.elapsed_time(e1) / 10, 4), "uncertified": unc,
+                          "stride_bigk": os.environ.get("MRAG_K7_STRIDE_BIGK", "16")}), flush=True)
