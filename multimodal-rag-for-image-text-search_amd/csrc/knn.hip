@@ -1003,6 +1003,14 @@ __device__ __forceinline__ void wave_merge_lowest(uint64_t (&run)[P], const uint
   }
 }
 
+#ifdef MRAG_K7_STAMPS
+// Diagnostic build only: K8 phase times (s_memtime of wave 0) per workgroup, [block][8]
+constexpr int K8_NSTAMP = 8, K8_MAXBLK = 4096;
+__device__ unsigned long long g_k8_stamps[K8_MAXBLK * K8_NSTAMP];
+#define K8_STAMP(i) k8t[i] = __builtin_amdgcn_s_memtime()
+#else
+#define K8_STAMP(i)
+#endif
 // K8: merge split lists, rescore exactly, certify. One workgroup per query.
 // SEL = 0: bitonic sort of all S KL keys in LDS. SEL = P > 0 (when M + 1 <= 64 P): only the
 // 64 P best keys are kept — every wave folds its share of the lists, 64 P keys at a time, into
@@ -1019,25 +1027,38 @@ __global__ __launch_bounds__(MERGE_THREADS) void knn_merge_kernel(MergeParams p)
 
   const int q = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+#ifdef MRAG_K7_STAMPS
+  unsigned long long k8t[K8_NSTAMP] = {};
+#endif
+  K8_STAMP(0);
 
   float tau = -INFINITY;
   int valid = 0;
   const int ntot = p.splits * p.KL;
-  auto load_key = [&](int e) -> uint64_t {  // candidate e of the union; invalid -> ~0 (sorts last)
-    uint64_t key = ~0ull;
-    if (e < ntot) {
-      const int sp = e / p.KL, j = e - sp * p.KL;
-      const size_t o = ((size_t)sp * p.Qp + q) * p.KL + j;
-      const int r = p.part_i[o];
-      if (r >= 0) {
-        const float s = p.part_s[o];
-        key = ((uint64_t)(~mrag_f2ord(s)) << 32) | (uint32_t)r;
-        ++valid;
-        if (j == p.KL - 1) tau = fmaxf(tau, s);
-      }
-    }
-    return key;
+  // candidate e of the union: the row and score are read together and unconditionally (a
+  // clamped slot past the union), so a chunk costs one memory round trip and the next chunk's
+  // reads can be in flight during this one's sort; invalid -> ~0 (sorts last)
+  struct Raw {
+    int r;
+    float s;
   };
+  auto load_raw = [&](int e) -> Raw {
+    const int ec = e < ntot ? e : 0;
+    const int sp = ec / p.KL, j = ec - sp * p.KL;
+    const size_t o = ((size_t)sp * p.Qp + q) * p.KL + j;
+    return Raw{p.part_i[o], p.part_s[o]};
+  };
+  auto make_key = [&](int e, Raw v) -> uint64_t {
+    if (e >= ntot || v.r < 0) return ~0ull;
+    ++valid;
+    if (e % p.KL == p.KL - 1) tau = fmaxf(tau, v.s);
+    return ((uint64_t)(~mrag_f2ord(v.s)) << 32) | (uint32_t)v.r;
+  };
+  auto load_key = [&](int e) -> uint64_t { return make_key(e, load_raw(e)); };
+  // the splits' drop bounds and the query row first: their reads overlap the key fold
+  if (p.part_tau)
+    for (int sp = tid; sp < p.splits; sp += MERGE_THREADS) tau = fmaxf(tau, p.part_tau[(size_t)sp * p.Qp + q]);
+  for (int d = tid; d < p.DP; d += MERGE_THREADS) qs[d] = p.q32[(size_t)q * p.DP + d];
   if constexpr (SEL == 0) {
     for (int e = tid; e < p.R; e += MERGE_THREADS) keys[e] = load_key(e);
   } else {
@@ -1045,19 +1066,28 @@ __global__ __launch_bounds__(MERGE_THREADS) void knn_merge_kernel(MergeParams p)
     uint64_t run[SEL];
 #pragma unroll
     for (int pp = 0; pp < SEL; ++pp) run[pp] = ~0ull;
-    for (int c = wave; c * E < ntot; c += MERGE_THREADS / 64) {  // wave-uniform
+    // software-pipelined: chunk c + 4's reads are issued before chunk c's sort (the reads, not
+    // the sorts, bounded the fold: 42k -> 37k cycles for the eight chunks a wave folds in a
+    // Q = 1 search; folding two chunks per step measured 35k there but slower at Q = 1000;
+    // profiles/r3_k8_stamps_*.log)
+    constexpr int NW = MERGE_THREADS / 64;
+    Raw nx[SEL];
+#pragma unroll
+    for (int pp = 0; pp < SEL; ++pp) nx[pp] = load_raw(wave * E + 64 * pp + lane);
+    for (int c = wave; c * E < ntot; c += NW) {  // wave-uniform
       uint64_t ch[SEL];
 #pragma unroll
-      for (int pp = 0; pp < SEL; ++pp) ch[pp] = load_key(c * E + 64 * pp + lane);
+      for (int pp = 0; pp < SEL; ++pp) {
+        ch[pp] = make_key(c * E + 64 * pp + lane, nx[pp]);
+        nx[pp] = load_raw((c + NW) * E + 64 * pp + lane);
+      }
       wave_sort_keys<SEL>(ch, lane);
       wave_merge_lowest<SEL>(run, ch, lane);
     }
 #pragma unroll
     for (int pp = 0; pp < SEL; ++pp) keys[wave * E + 64 * pp + lane] = run[pp];
   }
-  if (p.part_tau)
-    for (int sp = tid; sp < p.splits; sp += MERGE_THREADS) tau = fmaxf(tau, p.part_tau[(size_t)sp * p.Qp + q]);
-  for (int d = tid; d < p.DP; d += MERGE_THREADS) qs[d] = p.q32[(size_t)q * p.DP + d];
+  K8_STAMP(1);
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
     tau = fmaxf(tau, __shfl_xor(tau, off));
@@ -1107,7 +1137,9 @@ __global__ __launch_bounds__(MERGE_THREADS) void knn_merge_kernel(MergeParams p)
       for (int pp = 0; pp < SEL; ++pp) keys[64 * pp + lane] = run[pp];
     }
   }
+  K8_STAMP(2);
   __syncthreads();
+  K8_STAMP(3);
 
   const int M = min(p.M, valid);
   const float a_next = (valid > M) ? mrag_ord2f(~(uint32_t)(keys[M] >> 32)) : -INFINITY;
@@ -1136,8 +1168,37 @@ __global__ __launch_bounds__(MERGE_THREADS) void knn_merge_kernel(MergeParams p)
       }
     }
   }
+  K8_STAMP(4);
+  if (p.Mp <= 64) {
+    // (ex, er) by (score desc, row asc), empty slots last: one wave's bitonic network in
+    // registers (the block-wide network below pays a barrier per stage: 13.3k -> 7.0k cycles,
+    // profiles/r3_k8_stamps_variants.log)
+    __syncthreads();
+    if (wave == 0) {
+      double sv = lane < p.Mp ? ex[lane] : -INFINITY;
+      int rv = lane < p.Mp ? er[lane] : -1;
+#pragma unroll
+      for (int size = 2; size <= 64; size <<= 1) {
+#pragma unroll
+        for (int st = size >> 1; st > 0; st >>= 1) {
+          const double so = __shfl_xor(sv, st);
+          const int ro = __shfl_xor(rv, st);
+          const bool asc = (lane & size) == 0, lower = (lane & st) == 0;
+          // the lower slot of an ascending pair keeps the one that ranks first
+          if (mrag_before(so, ro, sv, rv) == (lower == asc)) {
+            sv = so;
+            rv = ro;
+          }
+        }
+      }
+      if (lane < p.Mp) {
+        ex[lane] = sv;
+        er[lane] = rv;
+      }
+    }
+  }
   // bitonic sort of (ex, er) by (score desc, row asc); empty slots last
-  for (int size = 2; size <= p.Mp; size <<= 1) {
+  for (int size = 2; size <= (p.Mp <= 64 ? 1 : p.Mp); size <<= 1) {
     for (int stride = size >> 1; stride > 0; stride >>= 1) {
       __syncthreads();
       for (int i = tid; i < (p.Mp >> 1); i += MERGE_THREADS) {
@@ -1156,6 +1217,7 @@ __global__ __launch_bounds__(MERGE_THREADS) void knn_merge_kernel(MergeParams p)
     }
   }
   __syncthreads();
+  K8_STAMP(5);
 
   for (int j = tid; j < p.k; j += MERGE_THREADS) {
     const bool has = j < M;
@@ -1178,6 +1240,11 @@ __global__ __launch_bounds__(MERGE_THREADS) void knn_merge_kernel(MergeParams p)
       p.fail_list[s] = q;
     }
   }
+#ifdef MRAG_K7_STAMPS
+  K8_STAMP(6);
+  if (tid == 0 && q < K8_MAXBLK)
+    for (int i = 0; i < K8_NSTAMP; ++i) g_k8_stamps[(size_t)q * K8_NSTAMP + i] = k8t[i];
+#endif
 }
 
 struct FinalParams {
@@ -1676,6 +1743,13 @@ int grow(mrag_knn_index* ix, int64_t need) {
 extern "C" {
 #ifdef MRAG_K7_STAMPS
 // diagnostic build only: copy the per-wave K7 segment sums of the last scan (n <= 2^16 * 8)
+// K8 phase stamps of the last merge: [block][8] s_memtime values (see knn_merge_kernel)
+__attribute__((visibility("default"))) int mrag_debug_k8_stamps(unsigned long long* out, int n) {
+  if (n > K8_MAXBLK * K8_NSTAMP) n = K8_MAXBLK * K8_NSTAMP;
+  MRAG_HIP(hipDeviceSynchronize());
+  MRAG_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_k8_stamps), (size_t)n * 8, 0, hipMemcpyDeviceToHost));
+  return MRAG_OK;
+}
 __attribute__((visibility("default"))) int mrag_debug_k7_stamps(unsigned long long* out, int n) {
   if (n > K7_MAXWAVES * K7_NSTAMP) n = K7_MAXWAVES * K7_NSTAMP;
   MRAG_HIP(hipDeviceSynchronize());
