@@ -77,6 +77,23 @@ def test_clusters_duplicates_ties(cuda):
     assert unc > 0, "expected the dense clusters to defeat the fp16 certificate"
 
 
+def test_collect_pass_many_failing_queries(cuda):
+    """More uncertified queries than one collect workgroup holds (256): K7c's grid is sized on
+    the host from the failure count read after K8 (several query groups x its own splits)."""
+    from app.vector_store import FlatIndex
+
+    x = clustered_corpus(30000, 512, 11, n_clusters=8, spread=0.01, dup_frac=0.2)
+    q = x[np.random.default_rng(5).integers(0, len(x), 640)] + 0.001
+    ix = FlatIndex(512)
+    ix.add(x)
+    s, r = ix.search(q, 50)
+    unc, _ = ix.last_stats()
+    os_, or_ = flat_cosine_topk(x, np.zeros(len(x)), q, 50)
+    _check(s, r, os_, or_)
+    assert unc > 0, "expected the dense clusters to defeat the fp16 certificate"
+    print(f"uncertified queries: {unc} (collect groups: {(unc + 255) // 256})")
+
+
 def test_many_exact_ties_overflow_retry(cuda):
     """5000 identical rows: the collect pass must grow past its default capacity."""
     from app.vector_store import FlatIndex
