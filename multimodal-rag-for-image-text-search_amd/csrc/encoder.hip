@@ -369,14 +369,6 @@ int clip_layer_pooled(mrag_encoder* e, const Layer& L, int B, int T, const int32
   return gemm(e->FG.p, L.w2.p, L.b2.p, XG, B, D, I, D, EPI_F32_RESIDUAL, s);
 }
 
-bool full_last_layer() {
-  static const bool v = [] {
-    const char* e = getenv("MRAG_ENC_FULL_LAST");
-    return e && atoi(e) == 1;
-  }();
-  return v;
-}
-
 // Post-LN transformer layer (BERT): X = LN(X + attn(X)); X = LN(X + ffn(X)).
 // Invariant on entry and exit: X (f32) and H16 == f16(X).
 int bert_layer(mrag_encoder* e, const Layer& L, int B, int T, const int32_t* mask, hipStream_t s) {
@@ -630,7 +622,7 @@ int mrag_encoder_embed_images(mrag_encoder* e, const uint8_t* images, int32_t ba
                                    (const float*)e->pre_g.p, (const float*)e->pre_b.p, X, B, T, D, c.ln_eps, s))
     return rc;
   if (int rc = launch_cls_rows(B, T, (int*)e->ROWS.p, s)) return rc;
-  const bool prune = !full_last_layer() && c.layers > 0;
+  const bool prune = c.layers > 0;
   for (int i = 0; i < c.layers; ++i) {
     if (prune && i == c.layers - 1) {
       if (int rc = clip_layer_pooled(e, e->layers[i], B, T, nullptr, 0, (const int*)e->ROWS.p, s)) return rc;
@@ -699,7 +691,7 @@ int mrag_encoder_embed_tokens(mrag_encoder* e, const int32_t* ids, const int32_t
                                     c.vocab, s))
       return rc;
     if (int rc = launch_eos_rows(dids, B, T, c.eos_token_id, (int*)e->ROWS.p, s)) return rc;
-    const bool prune = !full_last_layer() && c.layers > 0;
+    const bool prune = c.layers > 0;
     for (int i = 0; i < c.layers; ++i) {
       if (prune && i == c.layers - 1) {
         if (int rc = clip_layer_pooled(e, e->layers[i], B, T, dmask, 1, (const int*)e->ROWS.p, s)) return rc;

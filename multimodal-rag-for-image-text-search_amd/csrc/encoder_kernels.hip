@@ -1265,11 +1265,7 @@ int launch_attention(const AttentionArgs& a, int dh, hipStream_t s) {
   MRAG_REQUIRE(dh == 64 || dh == 32, "attention: head_dim %d unsupported (32, 64)", dh);
   const int64_t items = (int64_t)a.B * a.H * ((a.L + 15) / 16);
   MRAG_REQUIRE(items < (1ll << 33), "attention: batch too large");
-  static const bool seq64 = [] {
-    const char* e = getenv("MRAG_ATTN_SEQ64");
-    return !(e && atoi(e) == 0);
-  }();
-  if (seq64 && a.L > 32 && a.L <= 64) {  // one workgroup per (sequence, head): the ViT's 50 tokens
+  if (a.L > 32 && a.L <= 64) {  // one workgroup per (sequence, head): the ViT's 50 tokens
     hipLaunchKernelGGL(dh == 64 ? attention_seq64_kernel<64> : attention_seq64_kernel<32>,
                        dim3((unsigned)((int64_t)a.B * a.H)), dim3(256), 0, s, a);
   } else {

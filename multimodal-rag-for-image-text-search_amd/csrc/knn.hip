@@ -1565,27 +1565,13 @@ scan_fn get_scan3(int DP, bool sample, int qb) {
 }
 
 // Query blocks per wave of the v3 scan for a batch: 1 (K7s, 64 queries per workgroup) while the
-// padded batch fits one small group, else 4 (256 per workgroup).
-int scan3_qb(int64_t nq) {
-  static const int small_max = [] {  // env MRAG_SCAN_SMALLQ (experiment): largest batch on K7s
-    const char* e = getenv("MRAG_SCAN_SMALLQ");
-    return e ? atoi(e) : 64;
-  }();
-  return nq <= small_max ? 1 : 4;
-}
+// batch fits one small group, else 4 (256 per workgroup).
+int scan3_qb(int64_t nq) { return nq <= 64 ? 1 : 4; }
 
 // Sample pre-pass stride for k: the main scan's fires grow with the rows above the seed, about
 // k x stride, so k > 16 samples every 4th tile (512k x 512, k = 50: search 0.824 -> 0.736 ms,
-// scan 0.659 -> 0.501; stride 8: 0.748; notes/knn_scan_experiments.md). Env
-// MRAG_K7_STRIDE_BIGK (experiment) sets the k > 16 stride.
-int sample_stride_for(int k) {
-  static const int big = [] {
-    const char* e = getenv("MRAG_K7_STRIDE_BIGK");
-    const int v = e ? atoi(e) : 4;
-    return v >= 2 && v <= 64 ? v : 4;
-  }();
-  return k > 16 ? big : SAMPLE_STRIDE;
-}
+// scan 0.659 -> 0.501; stride 8: 0.748; notes/knn_scan_experiments.md).
+int sample_stride_for(int k) { return k > 16 ? 4 : SAMPLE_STRIDE; }
 
 scan_fn get_scan(int DP, int KL, bool collect) {
   switch (DP) {
@@ -1632,6 +1618,10 @@ struct mrag_knn_index {
   std::mutex pool_mu;                        // guards the context pool and the stats below
   std::vector<SearchCtx*> ctx_all, ctx_free;
   int64_t last_uncertified = 0, last_retries = 0;
+  // diagnostics of the last search (mrag_debug_knn_last_collect): its context (buffers stay valid
+  // until that context's next search) and the grid it used
+  SearchCtx* last_ctx = nullptr;
+  int32_t last_info[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // S, Qp, cgroups, Sc, ccap, uncertified, overflow, KL
   // optional scan timing (mrag_knn_profile)
   bool profile = false;
   double scan_ms = 0.0;
@@ -1932,6 +1922,7 @@ int mrag_knn_search(mrag_knn_index* ix, const float* queries, int64_t nq, int32_
     }
   }
   int64_t uncertified = 0, retries = 0;
+  int32_t info[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 
   auto generic_args = [&]() {
     mrag_knn::GenericSearch ga{};
@@ -1995,6 +1986,9 @@ int mrag_knn_search(mrag_knn_index* ix, const float* queries, int64_t nq, int32_
     const int M = std::min<int>(k + 32, S * KL);
     const int R = (int)next_pow2((int64_t)S * KL);
     const int Mp = (int)next_pow2(std::max(M, 2));
+    info[0] = S;
+    info[1] = (int32_t)Qp;
+    info[7] = KL;
 
     const float* qsrc = queries;
     if (host) {
@@ -2133,6 +2127,10 @@ int mrag_knn_search(mrag_knn_index* ix, const float* queries, int64_t nq, int32_
       if (Sc >= 8) Sc &= ~7;
       sp.qgroups = cgroups;
       sp.splits = Sc;
+      info[2] = cgroups;
+      info[3] = Sc;
+      info[4] = ccap;
+      info[5] = (int32_t)uncertified;
       hipLaunchKernelGGL(collect, dim3((unsigned)(cgroups * Sc)), dim3(SCAN_THREADS), 0, s, sp);
       MRAG_CHECK_LAUNCH();
       FinalParams fp{};
@@ -2158,6 +2156,7 @@ int mrag_knn_search(mrag_knn_index* ix, const float* queries, int64_t nq, int32_
       MRAG_CHECK_LAUNCH();
       MRAG_HIP(hipMemcpyAsync(c->host_counters, c->counters.p, 8, hipMemcpyDeviceToHost, s));
       if (int rc = wait_stream(c, s)) return rc;
+      info[6] = c->host_counters[1];
       if (c->host_counters[1] != 0) {
         retries = 1;
         if (int rc = mrag_knn::search_generic(generic_args(), c->gws, s, nullptr)) return rc;
@@ -2175,6 +2174,30 @@ int mrag_knn_search(mrag_knn_index* ix, const float* queries, int64_t nq, int32_
   std::lock_guard<std::mutex> lk(ix->pool_mu);
   ix->last_uncertified = uncertified;
   ix->last_retries = retries;
+  ix->last_ctx = c;
+  std::copy(info, info + 8, ix->last_info);
+  return MRAG_OK;
+}
+
+// Diagnostic (not in mrag.h): the collect-pass bookkeeping of the index's last search, for
+// scripts/knn_collect_diag.py. Valid only while no other search has run on the index since.
+// info[8] = S, Qp, cgroups, Sc, ccap, uncertified, overflow flag, KL; fail_list / cand_cnt get
+// the first `uncertified` slots, thresh the first `nthresh` queries (any pointer may be NULL).
+__attribute__((visibility("default"))) int mrag_debug_knn_last_collect(mrag_knn_index* ix, int32_t* info,
+                                                                       int32_t* fail_list, int32_t* cand_cnt,
+                                                                       float* thresh, int64_t nthresh) {
+  MRAG_REQUIRE(ix != nullptr && info != nullptr, "NULL argument");
+  std::lock_guard<std::mutex> lk(ix->pool_mu);
+  std::copy(ix->last_info, ix->last_info + 8, info);
+  SearchCtx* c = ix->last_ctx;
+  if (!c) return MRAG_OK;
+  mrag::DeviceGuard g(ix->device);
+  const int64_t unc = ix->last_info[5];
+  MRAG_HIP(hipDeviceSynchronize());
+  if (fail_list && unc > 0) MRAG_HIP(hipMemcpy(fail_list, c->fail_list.p, unc * 4, hipMemcpyDeviceToHost));
+  if (cand_cnt && unc > 0) MRAG_HIP(hipMemcpy(cand_cnt, c->cand_cnt.p, unc * 4, hipMemcpyDeviceToHost));
+  if (thresh && nthresh > 0 && (size_t)nthresh * 4 <= c->thresh.bytes)
+    MRAG_HIP(hipMemcpy(thresh, c->thresh.p, nthresh * 4, hipMemcpyDeviceToHost));
   return MRAG_OK;
 }
 
