@@ -724,7 +724,7 @@ def main():
                                          "ms_per_step": round(serial_dt / args.steps * 1e3, 4)},
             },
             "roofline": {
-                "kernel": "knn_scan3_kernel<512, 0, 0, 4> (K7 v3 main scan, MFMA 16x16x32; the 1/16 sample pre-pass is a separate launch, inside ms_per_step)",
+                "kernel": "knn_scan3_kernel<512, 0, 4> (K7 v3 main scan, MFMA 16x16x32; the 1/16 sample pre-pass is a separate launch, inside ms_per_step)",
                 "bound": "mfma",
                 "achieved": round(achieved_tflops, 2),
                 "peak": MFMA_FP16_PEAK_TFLOPS,

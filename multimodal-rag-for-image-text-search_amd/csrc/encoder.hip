@@ -326,7 +326,7 @@ int clip_layer(mrag_encoder* e, const Layer& L, int B, int T, const int32_t* mas
       return rc;
     }
   }
-  if (int rc = gemm(H, L.w1.p, L.b1.p, e->F16.p, M, I, D, I, act, s)) return rc;
+  if (int rc = gemm(H, L.w1.p, L.b1.p, e->F16.p, M, I, D, I, act, s, lib)) return rc;
   return gemm(e->F16.p, L.w2.p, L.b2.p, X, M, D, I, D, EPI_F32_RESIDUAL, s, lib);
 }
 

@@ -22,6 +22,11 @@ struct GemmArgs {
   int M, N, K, lda, ldw, ldc;
   int lib_ok;         // the call may run on hipBLASLt (plain epilogues, M >= 4096: blaslt.cpp)
   float alpha;        // C = alpha acc (+ ...): hipBLASLt only; 0 or 1 = none (K3 / K3d have none)
+  // K3d stream-K workspace (set by the launcher): f32 partial tiles [2 * grid][256 * 256], an
+  // arrival ticket per tile and a ready flag per partial slot (all zero between launches)
+  float* sk_part;
+  int* sk_cnt;
+  int* sk_flag;
 };
 
 struct LayerNormArgs {

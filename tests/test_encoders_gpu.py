@@ -213,8 +213,11 @@ def test_gemm_shapes_every_epilogue(cuda, gemm_library):
     import torch
     from app.encoders import gemm_nt
 
+    # (12800, 768, 768) / (12800, 768, 3072) / (12800, 3072, 768) / (11000, 768, 3072): K3d stream-K
+    # under the hand-written library (cut tiles of two and three pieces, ragged last row tile)
     for (M, N, K) in [(1100, 768, 768), (2100, 1536, 256), (12800, 768, 3072), (12800, 2304, 768),
-                      (300, 256, 64), (5000, 512, 2048), (16000, 384, 1536)]:
+                      (300, 256, 64), (5000, 512, 2048), (16000, 384, 1536), (12800, 768, 768),
+                      (12800, 3072, 768), (11000, 768, 3072)]:
         for epi in range(5):
             g = torch.Generator(device="cuda").manual_seed(epi + K)
             A = (torch.randn(M, K, generator=g, device="cuda") * 0.5).half()
