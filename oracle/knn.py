@@ -34,13 +34,54 @@ def cosine_scores(corpus: np.ndarray, queries: np.ndarray) -> np.ndarray:
     return cos
 
 
+def duplicate_groups(corpus: np.ndarray, block: int = 16384):
+    """Rows with identical f32 contents (exact duplicates: re-ingested chunks, repeated frames).
+
+    Returns (gid, reps): gid[row] = group index or -1 for a row without a duplicate, reps[g] =
+    the first row of group g. Found by an exact integer hash of the row bits (int64 wraparound,
+    deterministic per row) and confirmed byte for byte.
+    """
+    X = np.ascontiguousarray(corpus, dtype=np.float32)
+    n = X.shape[0]
+    gid = np.full(n, -1, dtype=np.int64)
+    if n < 2:
+        return gid, np.zeros(0, dtype=np.int64)
+    coef = np.random.default_rng(12345).integers(1, 2**62, size=X.shape[1], dtype=np.int64) | 1
+    h = np.empty(n, dtype=np.int64)
+    bits = X.view(np.int32)
+    with np.errstate(over="ignore"):
+        for b0 in range(0, n, block):
+            h[b0:b0 + block] = (bits[b0:b0 + block].astype(np.int64) * coef).sum(axis=1)
+    order = np.argsort(h, kind="stable")
+    hs = h[order]
+    starts = np.nonzero(np.r_[True, hs[1:] != hs[:-1]])[0]
+    ends = np.r_[starts[1:], n]
+    reps = []
+    for a, b in zip(starts, ends):
+        if b - a < 2:
+            continue
+        members = np.sort(order[a:b])
+        rest = members
+        while rest.size > 1:  # split a hash bucket into byte-identical groups
+            same = np.all(X[rest] == X[rest[0]], axis=1) & np.all(bits[rest] == bits[rest[0]], axis=1)
+            grp = rest[same]
+            if grp.size > 1:
+                gid[grp] = len(reps)
+                reps.append(int(grp[0]))
+            rest = rest[~same]
+    return gid, np.asarray(reps, dtype=np.int64)
+
+
 def flat_cosine_topk(corpus, labels, queries, k: int, label_filter: int = -1, row_offset: int = 0,
                      chunk: int = 131072):
     """Exact top-k. Returns (scores f64 [nq,k], rows int64 [nq,k]); empty slots -inf / -1.
 
     The corpus is scanned in chunks (bounded memory at 1M+ rows); every chunk keeps
     all rows scoring >= its own k-th score, so ties at the boundary survive to the
-    final (score desc, row asc) selection.
+    final (score desc, row asc) selection. Identical rows score identically (one BLAS
+    product per distinct vector: a blocked product may round the same dot product
+    differently at different column positions, ~1e-16, which would order exact
+    duplicates by position instead of by row).
     """
     corpus = np.asarray(corpus, dtype=np.float32)
     queries = np.asarray(queries, dtype=np.float32)
@@ -56,11 +97,17 @@ def flat_cosine_topk(corpus, labels, queries, k: int, label_filter: int = -1, ro
     all_rows = np.nonzero(mask)[0]
     if all_rows.size == 0:
         return out_s, out_r
+    gid, reps = duplicate_groups(corpus)
+    rep_cos = cosine_scores(corpus[reps], queries) if reps.size else None
     cand_s = [[] for _ in range(nq)]
     cand_r = [[] for _ in range(nq)]
     for c0 in range(0, all_rows.size, chunk):
         rows = all_rows[c0:c0 + chunk]
         cos = cosine_scores(corpus[rows], queries)
+        if rep_cos is not None:
+            dup = np.nonzero(gid[rows] >= 0)[0]
+            if dup.size:
+                cos[:, dup] = rep_cos[:, gid[rows[dup]]]
         kk = min(k, rows.size)
         for i in range(nq):
             s = cos[i]
