@@ -97,3 +97,28 @@ def test_knn_oracle_fixture_and_sklearn(tag):
     diff = idx != r
     if diff.any():
         assert np.all(np.abs((1.0 - dist)[diff] - s[diff]) < 1e-12)
+
+
+def test_knn_oracle_duplicates_tie_by_row():
+    """Exact duplicate rows must score bit-identically and come back in row order (the pinned
+    tie rule), wherever they sit in the corpus and across the oracle's scan chunks: a blocked
+    BLAS product can round one dot product differently at different column positions (~1e-16,
+    observed with 640 queries over 30k clustered rows, round 4), which would order duplicates
+    by position."""
+    from oracle.knn import duplicate_groups, flat_cosine_topk
+
+    x = clustered_corpus(30000, 512, 11, n_clusters=8, spread=0.01, dup_frac=0.2)
+    q = x[np.random.default_rng(5).integers(0, len(x), 640)] + np.float32(0.001)
+    gid, reps = duplicate_groups(x)
+    assert reps.size > 1000
+    for chunk in (131072, 7001):  # one chunk / duplicates split across chunks
+        s, r = flat_cosine_topk(x, np.zeros(len(x)), q, 50, chunk=chunk)
+        g = gid[r]
+        for i in range(len(q)):
+            for a in range(49):
+                if g[i, a] >= 0 and g[i, a] == g[i, a + 1]:
+                    assert s[i, a] == s[i, a + 1] and r[i, a] < r[i, a + 1]
+        if chunk == 131072:
+            first = (s, r)
+    np.testing.assert_array_equal(first[1], r)
+    np.testing.assert_allclose(first[0], s, rtol=0, atol=1e-14)  # other rows: ulps by chunking
