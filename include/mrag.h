@@ -223,17 +223,10 @@ int mrag_image_resize_crop(const uint8_t* pixels, const int64_t* offsets, const 
 
 /* K3 building block: C[M][N] (op)= A[M][K] . W[N][K]^T + bias (device pointers;
  * A, W fp16 row-major; epilogue 0 f16 out, 1 f16 quick_gelu, 2 f16 gelu_erf,
- * 3 f32 C += , 4 f32 out, 5 f16 swish = x sigmoid(x): the library only, M >= 4096, else
- * MRAG_ERR_UNSUPPORTED). N % 128 == 0, K % 64 == 0. */
+ * 3 f32 C += , 4 f32 out). N % 128 == 0, K % 64 == 0; bias and C 16-byte aligned. */
 int mrag_gemm_nt(const void* A, const void* W, const float* bias, void* C, int32_t M, int32_t N, int32_t K,
                  int32_t epilogue, void* stream);
 
-/* Which kernels run the CLIP image tower's plain GEMMs (epilogues 0, 3, 4: patch embed, q|k|v,
- * out-proj, fc2) and mrag_gemm_nt at M >= 4096 rows: 1 (the default) hipBLASLt, 0 the
- * hand-written K3 / K3d (also selected by MRAG_GEMM_BLASLT=0 in the environment). The activation
- * epilogues (1, 2), smaller M and the text towers always run K3 / K3d. Process-wide; set it
- * while no encoder call is in flight. Returns the previous mode. */
-int mrag_gemm_set_library(int32_t mode);
 
 #ifdef __cplusplus
 }

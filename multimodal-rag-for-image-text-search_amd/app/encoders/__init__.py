@@ -46,7 +46,6 @@ def _register_signatures():
         "mrag_encoder_embed_images": [vp, vp, i32, vp, i32, i32, vp],
         "mrag_encoder_embed_tokens": [vp, vp, vp, i32, i32, vp, i32, i32, vp],
         "mrag_gemm_nt": [vp, vp, vp, vp, i32, i32, i32, i32, vp],
-        "mrag_gemm_set_library": [i32],
         "mrag_encoder_score_pairs": [vp, vp, vp, vp, i32, i32, vp, i32, vp],
     }
     for name, args in sigs.items():
@@ -183,13 +182,6 @@ def gemm_nt(A, W, bias, C, epilogue: int):
     _native.check(lib.mrag_gemm_nt(A.data_ptr(), W.data_ptr(), bias.data_ptr() if bias is not None else None,
                                    C.data_ptr(), M, N, K, epilogue, stream), "mrag_gemm_nt")
     return C
-
-
-def set_gemm_library(mode: int) -> int:
-    """1: hipBLASLt runs the CLIP image tower's plain GEMMs (bias / residual / f32 epilogues) and
-    gemm_nt at >= 4096 rows (the default); 0: the hand-written K3 / K3d everywhere (the text towers
-    always). Returns the previous mode (mrag_gemm_set_library, include/mrag.h)."""
-    return int(_register_signatures().mrag_gemm_set_library(int(mode)))
 
 
 def load_encoder(cfg: EncoderConfig, model_name: Optional[str] = None, device: int = 0, seed: int = 0,

@@ -46,9 +46,7 @@ void buf_free(Buf& b) {
 
 struct Layer {
   Buf wqkv, bqkv, wo, bo, w1, b1, w2, b2, ln1g, ln1b, ln2g, ln2b;
-  Buf b1s;  // image tower: QUICK_GELU_SLOPE * b1 (fc1 as the library's swish, clip_layer)
 };
-constexpr float QUICK_GELU_SLOPE = 1.702f;  // quick_gelu(z) = z sigmoid(1.702 z) = swish(1.702 z) / 1.702
 
 __global__ void f32_to_f16_kernel(const float* __restrict__ in, _Float16* __restrict__ out, int64_t n) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -260,10 +258,8 @@ int ensure_workspace(mrag_encoder* e, int B, int T) {
 
 // GEMM helper: C = A[M][K] . W[N][K]^T (+bias), epilogue
 int gemm(const void* A, const void* W, const void* bias, void* C, int M, int N, int K, int ldc, int epi,
-         hipStream_t s, bool lib_ok = false, float alpha = 0.f) {
+         hipStream_t s) {
   GemmArgs g{};
-  g.lib_ok = lib_ok ? 1 : 0;
-  g.alpha = alpha;
   g.A = (const _Float16*)A;
   g.W = (const _Float16*)W;
   g.bias = (const float*)bias;
@@ -297,11 +293,10 @@ int layernorm(const float* x, const int* gather, float* y32, _Float16* y16, cons
 int clip_layer(mrag_encoder* e, const Layer& L, int B, int T, const int32_t* mask, int causal, hipStream_t s) {
   const auto& c = e->cfg;
   const int D = c.hidden, I = c.intermediate, M = B * T;
-  const bool lib = c.image_size > 0;  // the image tower's plain GEMMs may run on hipBLASLt
   float* X = (float*)e->X.p;
   _Float16* H = (_Float16*)e->H16.p;
   if (int rc = layernorm(X, nullptr, nullptr, H, L.ln1g, L.ln1b, M, D, c.ln_eps, s)) return rc;
-  if (int rc = gemm(H, L.wqkv.p, L.bqkv.p, e->QKV.p, M, 3 * D, D, 3 * D, EPI_F16, s, lib)) return rc;
+  if (int rc = gemm(H, L.wqkv.p, L.bqkv.p, e->QKV.p, M, 3 * D, D, 3 * D, EPI_F16, s)) return rc;
   AttentionArgs a{};
   a.qkv = (const _Float16*)e->QKV.p;
   a.out = (_Float16*)e->ATT.p;
@@ -312,22 +307,11 @@ int clip_layer(mrag_encoder* e, const Layer& L, int B, int T, const int32_t* mas
   a.causal = causal;
   a.scale = 1.0f / sqrtf((float)(D / c.heads));
   if (int rc = launch_attention(a, D / c.heads, s)) return rc;
-  if (int rc = gemm(e->ATT.p, L.wo.p, L.bo.p, X, M, D, D, D, EPI_F32_RESIDUAL, s, lib)) return rc;
+  if (int rc = gemm(e->ATT.p, L.wo.p, L.bo.p, X, M, D, D, D, EPI_F32_RESIDUAL, s)) return rc;
   if (int rc = layernorm(X, nullptr, nullptr, H, L.ln2g, L.ln2b, M, D, c.ln_eps, s)) return rc;
   const int act = c.act == 0 ? EPI_F16_QUICK_GELU : EPI_F16_GELU_ERF;
-  if (lib && c.act == 0 && L.b1s.p && blaslt_takes(M)) {
-    // the MLP on the library: F16 = swish(1.702 (H W1^T + b1)) = 1.702 quick_gelu(...), then
-    // X += (1 / 1.702) F16 W2^T + b2 (the bias is not scaled by alpha)
-    int rc = gemm(H, L.w1.p, L.b1s.p, e->F16.p, M, I, D, I, EPI_F16_SWISH_LIB, s, true, QUICK_GELU_SLOPE);
-    if (rc == MRAG_OK) {
-      rc = gemm(e->F16.p, L.w2.p, L.b2.p, X, M, D, I, D, EPI_F32_RESIDUAL, s, true, 1.0f / QUICK_GELU_SLOPE);
-      if (rc != MRAG_ERR_UNSUPPORTED) return rc;  // else: fc1 again by hand below, fc2 with it
-    } else if (rc != MRAG_ERR_UNSUPPORTED) {
-      return rc;
-    }
-  }
-  if (int rc = gemm(H, L.w1.p, L.b1.p, e->F16.p, M, I, D, I, act, s, lib)) return rc;
-  return gemm(e->F16.p, L.w2.p, L.b2.p, X, M, D, I, D, EPI_F32_RESIDUAL, s, lib);
+  if (int rc = gemm(H, L.w1.p, L.b1.p, e->F16.p, M, I, D, I, act, s)) return rc;
+  return gemm(e->F16.p, L.w2.p, L.b2.p, X, M, D, I, D, EPI_F32_RESIDUAL, s);
 }
 
 // The LAST pre-LN layer of a tower that pools one row per sequence (CLIP: the class token of
@@ -336,19 +320,16 @@ int clip_layer(mrag_encoder* e, const Layer& L, int B, int T, const int32_t* mas
 // `rows`, gathered into XG (f32 residual) / AG (attention output). A GEMM row, a LayerNorm row
 // and the residual add depend only on that row (every hand-written GEMM kernel accumulates in
 // one order whatever M selects it), so the pooled rows are bit-identical to the full layer's
-// under the hand-written kernels (mrag_gemm_set_library(0); the image tower's full-layer M >=
-// 4096 GEMMs otherwise run on hipBLASLt, another order) (env MRAG_ENC_FULL_LAST=1 runs the full
-// layer: A/B check in scripts/enc_dump.py). ViT-B/32 at
+// (A/B check against the full layer in scripts/enc_dump.py). ViT-B/32 at
 // B = 256: the layer's out-proj / fc1 / fc2 run on 256 rows instead of 12,800.
 int clip_layer_pooled(mrag_encoder* e, const Layer& L, int B, int T, const int32_t* mask, int causal, const int* rows,
                       hipStream_t s) {
   const auto& c = e->cfg;
   const int D = c.hidden, I = c.intermediate, M = B * T;
-  const bool lib = c.image_size > 0;  // the image tower's plain GEMMs may run on hipBLASLt
   float* X = (float*)e->X.p;
   _Float16* H = (_Float16*)e->H16.p;
   if (int rc = layernorm(X, nullptr, nullptr, H, L.ln1g, L.ln1b, M, D, c.ln_eps, s)) return rc;
-  if (int rc = gemm(H, L.wqkv.p, L.bqkv.p, e->QKV.p, M, 3 * D, D, 3 * D, EPI_F16, s, lib)) return rc;
+  if (int rc = gemm(H, L.wqkv.p, L.bqkv.p, e->QKV.p, M, 3 * D, D, 3 * D, EPI_F16, s)) return rc;
   AttentionArgs a{};
   a.qkv = (const _Float16*)e->QKV.p;
   a.out = (_Float16*)e->ATT.p;
@@ -455,8 +436,7 @@ int mrag_encoder_destroy(mrag_encoder* e) {
     if (e->done) (void)hipEventDestroy(e->done);
     if (e->null_ev) (void)hipEventDestroy(e->null_ev);
     for (auto& L : e->layers)
-      for (Buf* b : {&L.wqkv, &L.bqkv, &L.wo, &L.bo, &L.w1, &L.b1, &L.w2, &L.b2, &L.ln1g, &L.ln1b, &L.ln2g, &L.ln2b,
-                     &L.b1s})
+      for (Buf* b : {&L.wqkv, &L.bqkv, &L.wo, &L.bo, &L.w1, &L.b1, &L.w2, &L.b2, &L.ln1g, &L.ln1b, &L.ln2g, &L.ln2b})
         buf_free(*b);
     for (Buf* b : {&e->patch_w, &e->cls, &e->pos, &e->pre_g, &e->pre_b, &e->post_g, &e->post_b, &e->proj_w, &e->tok,
                    &e->type0, &e->emb_g, &e->emb_b, &e->X, &e->H16, &e->QKV, &e->ATT, &e->F16, &e->PATCH, &e->IMG,
@@ -506,12 +486,6 @@ int mrag_encoder_set_param(mrag_encoder* e, const char* cname, const float* data
       rc = is_w ? upload(L.wo, data, numel, true, s) : upload(L.bo, data, numel, false, s);
     } else if (name.find("fc1") != std::string::npos || name.find("intermediate.dense") != std::string::npos) {
       rc = is_w ? upload(L.w1, data, numel, true, s) : upload(L.b1, data, numel, false, s);
-      if (rc == MRAG_OK && !is_w && c.image_size > 0 && c.act == 0) {  // image tower: the swish-form bias
-        std::vector<float> sc((size_t)numel);
-        for (int64_t i = 0; i < numel; ++i) sc[(size_t)i] = QUICK_GELU_SLOPE * data[i];
-        rc = upload(L.b1s, sc.data(), numel, false, s);
-        if (rc == MRAG_OK) MRAG_HIP(hipStreamSynchronize(s));  // sc is a host temporary
-      }
     } else if (name.find("fc2") != std::string::npos || name.find("output.dense") != std::string::npos) {
       rc = is_w ? upload(L.w2, data, numel, true, s) : upload(L.b2, data, numel, false, s);
     } else if (name.find("layer_norm1") != std::string::npos ||
@@ -617,7 +591,7 @@ int mrag_encoder_embed_images(mrag_encoder* e, const uint8_t* images, int32_t ba
   }
   float* X = (float*)e->X.p;
   if (int rc = launch_vit_im2col(img, (_Float16*)e->F16.p, B, S, P, s)) return rc;
-  if (int rc = gemm(e->F16.p, e->patch_w.p, nullptr, e->PATCH.p, B * (T - 1), D, Kp, D, EPI_F32, s, true)) return rc;
+  if (int rc = gemm(e->F16.p, e->patch_w.p, nullptr, e->PATCH.p, B * (T - 1), D, Kp, D, EPI_F32, s)) return rc;
   if (int rc = launch_vit_embed_ln((const float*)e->PATCH.p, (const float*)e->cls.p, (const float*)e->pos.p,
                                    (const float*)e->pre_g.p, (const float*)e->pre_b.p, X, B, T, D, c.ln_eps, s))
     return rc;
@@ -794,9 +768,7 @@ int mrag_gemm_nt(const void* A, const void* W, const float* bias, void* C, int32
                  int32_t epilogue, void* stream) {
   MRAG_REQUIRE(A && W && C, "NULL pointer");
   MRAG_REQUIRE(M >= 0 && N > 0 && K > 0, "bad shape");
-  return gemm(A, W, bias, C, M, N, K, N, epilogue, (hipStream_t)stream, /*lib_ok=*/true);
+  return gemm(A, W, bias, C, M, N, K, N, epilogue, (hipStream_t)stream);
 }
-
-int mrag_gemm_set_library(int32_t mode) { return mrag_enc::set_blaslt_mode(mode); }
 
 }  // extern "C"

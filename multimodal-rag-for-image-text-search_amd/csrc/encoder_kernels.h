@@ -11,7 +11,6 @@ enum Epilogue {
   EPI_F16_GELU_ERF = 2,    // C16 = gelu_erf(acc + bias)         (BERT intermediate)
   EPI_F32_RESIDUAL = 3,    // C32 += acc + bias                  (out-proj / fc2 into the residual)
   EPI_F32 = 4,             // C32 = acc + bias                   (patch embed, projections)
-  EPI_F16_SWISH_LIB = 5,   // C16 = swish(alpha acc + bias), hipBLASLt only (image-tower fc1, blaslt.cpp)
 };
 
 struct GemmArgs {
@@ -20,13 +19,6 @@ struct GemmArgs {
   const float* bias;  // [N] or null
   void* C;            // [M][ldc] f16 or f32 per epilogue
   int M, N, K, lda, ldw, ldc;
-  int lib_ok;         // the call may run on hipBLASLt (plain epilogues, M >= 4096: blaslt.cpp)
-  float alpha;        // C = alpha acc (+ ...): hipBLASLt only; 0 or 1 = none (K3 / K3d have none)
-  // K3d stream-K workspace (set by the launcher): f32 partial tiles [2 * grid][256 * 256], an
-  // arrival ticket per tile and a ready flag per partial slot (all zero between launches)
-  float* sk_part;
-  int* sk_cnt;
-  int* sk_flag;
 };
 
 struct LayerNormArgs {
@@ -49,11 +41,6 @@ struct AttentionArgs {
 };
 
 int launch_gemm(const GemmArgs& g, int epi, hipStream_t s);
-// plain epilogues (bias, residual, f32) on hipBLASLt where selected (blaslt.cpp)
-bool blaslt_eligible(const GemmArgs& g, int epi);
-bool blaslt_takes(int M);  // the library is selected and M is large enough (image tower)
-int set_blaslt_mode(int mode);
-int launch_gemm_blaslt(const GemmArgs& g, int epi, hipStream_t s);
 int launch_layernorm(const LayerNormArgs& a, hipStream_t s);
 int launch_attention(const AttentionArgs& a, int dh, hipStream_t s);
 int launch_vit_im2col(const uint8_t* img, _Float16* out, int B, int S, int P, hipStream_t s);

@@ -13,8 +13,6 @@
 #include <algorithm>
 #include <type_traits>
 #include <cstdlib>
-#include <map>
-#include <mutex>
 
 #include "common.h"
 #include "encoder_kernels.h"
@@ -22,7 +20,6 @@
 #define AS3 __attribute__((address_space(3)))
 
 namespace mrag_enc {
-using mrag::static_for;
 
 __device__ __forceinline__ void glds_x4(const void* gsrc, uint32_t lds_addr) {
   unsigned keep;
@@ -127,6 +124,24 @@ __device__ __forceinline__ void gemm_store8(const GemmArgs& g, int m, int n, f32
   }
 }
 
+// gemm_store8 for the f32 residual epilogue with the old C values already loaded (the epilogues
+// load a batch of C blocks before storing any: a store may alias a later load, so loads issued
+// block by block between the stores cost one memory round trip per block). Same arithmetic:
+// C = C + (acc + bias).
+__device__ __forceinline__ void gemm_store8_res(const GemmArgs& g, int m, int n, f32x4 v0, f32x4 v1,
+                                                const float* bn, f32x4 c0, f32x4 c1) {
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    v0[r] += bn[r];
+    v1[r] += bn[4 + r];
+    c0[r] += v0[r];
+    c1[r] += v1[r];
+  }
+  f32x4* p = (f32x4*)((float*)g.C + (size_t)m * g.ldc + n);
+  p[0] = c0;
+  p[1] = c1;
+}
+
 __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   // blocks bid, bid+8, ... share an XCD; give each XCD a contiguous range of tile ids
   const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
@@ -220,16 +235,43 @@ __global__ __launch_bounds__(GTHREADS) void gemm_nt_kernel(GemmArgs g) {
     __syncthreads();
   }
 
+  // epilogue: bias as one 16-byte load per column block; for the residual, every old C block of
+  // the wave in one batch of loads (rows clamped into the matrix) before the first store — loads
+  // issued between stores that may alias them cost one memory round trip per block
+  f32x4 bv[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) bv[j] = f32x4{};
+  if (g.bias) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bv[j] = *(const f32x4*)(g.bias + n0 + wc * 64 + 16 * j + 4 * fq);
+  }
+  f32x4 cv[4][4];
+  if constexpr (EPI == EPI_F32_RESIDUAL) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int mc = min(m0 + wr * 64 + 16 * i + fr, g.M - 1);
+        cv[i][j] = *(const f32x4*)((const float*)g.C + (size_t)mc * g.ldc + n0 + wc * 64 + 16 * j + 4 * fq);
+      }
+  }
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int n = n0 + wc * 64 + 16 * j + 4 * fq;
-    float bn[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) bn[r] = g.bias ? g.bias[n + r] : 0.f;
+    const float bn[4] = {bv[j][0], bv[j][1], bv[j][2], bv[j][3]};
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int m = m0 + wr * 64 + 16 * i + fr;
-      if (m < g.M) gemm_store4<EPI>(g, m, n, acc[i][j], bn);
+      if (m < g.M) {
+        if constexpr (EPI == EPI_F32_RESIDUAL) {
+          f32x4 c = cv[i][j], v = acc[i][j];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) c[r] += v[r] + bn[r];
+          *(f32x4*)((float*)g.C + (size_t)m * g.ldc + n) = c;
+        } else {
+          gemm_store4<EPI>(g, m, n, acc[i][j], bn);
+        }
+      }
     }
   }
 }
@@ -317,36 +359,20 @@ __device__ __forceinline__ void vmcnt_wait_c() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-// SK = 1: stream-K (the image tower's large batches, where 256 x 256 tiles leave CUs idle: ViT
-// out-proj / fc2 / patch embed run 150 tiles, fc1 600, on 256 CUs). The tiles of an XCD (the
-// contiguous range above) form one sequence of K-tile iterations, tile-major, cut into nbx equal
-// contiguous ranges, one per workgroup of that XCD; every workgroup walks its range forward, so
-// its first segment is the tail of a tile, then whole tiles, then the head of another. A tile cut
-// between workgroups is finished by the piece that ARRIVES LAST (agent-scope ticket per tile): an
-// earlier piece stores its raw accumulators to its slot (sc1 16-byte stores, drained) and sets the
-// slot's ready flag; the last one waits for the flags of pieces that took their tickets before it
-// (so it only ever waits on running workgroups: no deadlock with other grids holding CUs), sums
-// the pieces IN K ORDER with sc1 loads, resets the flags and the ticket, and runs the epilogue.
-// The sum order depends only on (M, N, K, grid), so a launch is deterministic; a row's last bits
-// differ from the one-accumulator order (the launcher uses SK for the image tower's large batches
-// only, whose rows the text-side bit-identity rule does not cover).
-constexpr int SK_SLOT_FLOATS = 256 * 256;
-
-template <int EPI, int SK>
+template <int EPI>
 __global__ __launch_bounds__(G8_THREADS) void gemm_8p_kernel(GemmArgs g) {
   using GG = G8Geom;
   constexpr int BM = GG::BM, BN = GG::BN, WM = GG::WM, WN = GG::WN, HM = GG::HM, HN = GG::HN;
   constexpr int NI = GG::NI, NJ = GG::NJ, PA = GG::PA, PB = GG::PB;
-  __shared__ __attribute__((aligned(16))) char smem[2 * G8_BUF + G8_BIAS_MAX * 4 + 16];
+  __shared__ __attribute__((aligned(16))) char smem[2 * G8_BUF + G8_BIAS_MAX * 4];
   float* sbias = (float*)(smem + 2 * G8_BUF);
-  int* sflag = (int*)(smem + 2 * G8_BUF + G8_BIAS_MAX * 4);
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wr = w >> 2, wc = w & 3;
   const int fr = lane & 15, fq = lane >> 4;
   const uint32_t lds_base = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)((AS3 char*)smem));
 
-  // this workgroup's tiles: lo + s + k * nbx, k = 0 .. my_n - 1 (SK: a range of K-tile iterations)
+  // this workgroup's tiles: lo + s + k * nbx, k = 0 .. my_n - 1
   const int tiles_n = g.N / BN;
   const int ntiles = ((g.M + BM - 1) / BM) * tiles_n;
   const int xcd = blockIdx.x & 7, sidx = blockIdx.x >> 3;
@@ -356,32 +382,20 @@ __global__ __launch_bounds__(G8_THREADS) void gemm_8p_kernel(GemmArgs g) {
   const int cnt = q8 + (xcd < r8 ? 1 : 0);
   const int my_n = sidx < cnt ? (cnt - sidx + nbx - 1) / nbx : 0;
   const int ktiles = g.K / GK;
-  const int64_t Ix = (int64_t)cnt * ktiles;  // SK: K-tile iterations of this XCD
-  auto range_lo = [&](int sx) -> int64_t { return (int64_t)sx * Ix / nbx; };
-  const int64_t it0 = SK ? range_lo(sidx) : 0, it1 = SK ? range_lo(sidx + 1) : 0;
-  const int t_first = SK ? (int)(it0 / ktiles) : 0;
-  const int nseg = SK ? (it1 > it0 ? (int)((it1 - 1) / ktiles) - t_first + 1 : 0) : my_n;
-  if (nseg == 0) return;  // whole workgroup, before any barrier
+  if (my_n == 0) return;  // whole workgroup, before any barrier
   // segment i of this workgroup: tile T, k-tiles [kb, ke)
   auto seg = [&](int i, int& T, int& kb, int& ke) {
-    if constexpr (SK) {
-      const int t = t_first + i;
-      const int64_t base = (int64_t)t * ktiles;
-      kb = (int)(it0 > base ? it0 - base : 0);
-      ke = (int)(it1 - base < ktiles ? it1 - base : ktiles);
-      T = lo + t;
-    } else {
-      T = lo + sidx + i * nbx;
-      kb = 0;
-      ke = ktiles;
-    }
+    T = lo + sidx + i * nbx;
+    kb = 0;
+    ke = ktiles;
   };
+  const int nseg = my_n;
 
   for (int i = threadIdx.x; i < g.N; i += G8_THREADS) sbias[i] = g.bias ? g.bias[i] : 0.f;
   __syncthreads();
 
-  const int KH = 4 * ktiles;                                        // half-tiles per tile
-  const int total = SK ? (int)(4 * (it1 - it0)) : my_n * KH;  // half-tiles of the whole stream
+  const int KH = 4 * ktiles;    // half-tiles per tile
+  const int total = my_n * KH;  // half-tiles of the whole stream
 
   // staging: a slot with PX pieces per wave gets pieces PX w .. PX w + PX - 1 (8 LDS rows each)
   // from this wave; LDS row j = 8 (PX w + q) + (lane >> 3), chunk position lane & 7 holds
@@ -535,105 +549,6 @@ __global__ __launch_bounds__(G8_THREADS) void gemm_8p_kernel(GemmArgs g) {
     vmcnt_wait(younger(1, last));  // L[0], L[1] landed
     bar();
   }
-  // SK: tile t (XCD-local; global id T) was cut and this workgroup holds one piece of it in acc.
-  // A piece that does not arrive last hands itself over; the last one sums the pieces in k order
-  // and stores the tile (the epilogue below, inlined: acc itself is never reassigned, which keeps
-  // the main loop's accumulators in place). See the SK note above the kernel.
-  auto sk_handoff = [&](int t, int T) {
-    if (wr == 0) bar();  // both wave groups at the same barrier count
-    if (threadIdx.x == 0) sflag[0] = atomicAdd(g.sk_cnt + T, 1);
-    __syncthreads();
-    const int ticket = sflag[0];
-    // the pieces of tile t: workgroups s_first .. s_last of this XCD, ascending s = ascending k
-    const int64_t b0 = (int64_t)t * ktiles, b1 = b0 + ktiles;
-    int s_first = (int)(b0 * nbx / Ix), s_last = (int)((b1 - 1) * nbx / Ix);
-    while (s_first + 1 < nbx && range_lo(s_first + 1) <= b0) ++s_first;
-    while (s_first > 0 && range_lo(s_first) > b0) --s_first;
-    while (s_last + 1 < nbx && range_lo(s_last + 1) <= b1 - 1) ++s_last;
-    while (s_last > 0 && range_lo(s_last) > b1 - 1) --s_last;
-    const int np = s_last - s_first + 1, me = sidx - s_first;
-    auto slot_of = [&](int sx) -> int {
-      return 2 * (xcd + 8 * sx) + (t == (int)(range_lo(sx) / ktiles) ? 0 : 1);
-    };
-    const __amdgpu_buffer_rsrc_t part = __builtin_amdgcn_make_buffer_rsrc(g.sk_part, 0, 0x7fffffff, 0x00020000);
-    const uint32_t tid16 = threadIdx.x * 16;
-    // chunk r = ((h * 2 + hh) * NI + i) * NJ + jb of a slot sits at r * 8 KiB + 16 * thread (the
-    // chunk offset goes in the instruction's scalar offset: one address VGPR per slot)
-    if (ticket < np - 1) {  // not last: hand the piece over
-      const uint32_t base = (uint32_t)slot_of(sidx) * (SK_SLOT_FLOATS * 4) + tid16;
-      static_for<32>([&](auto r_c) {
-        constexpr int r = decltype(r_c)::value, qq = r / (NI * NJ), i = (r % (NI * NJ)) / NJ, jb = r % NJ;
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[qq >> 1][qq & 1][i][jb]), part, base,
-                                               r * (G8_THREADS * 16), 16 /* sc1 */);
-      });
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's piece has left the CU
-      __syncthreads();
-      if (threadIdx.x == 0)
-        (void)__hip_atomic_fetch_add(g.sk_flag + slot_of(sidx), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return;
-    }
-    // last: every other piece took its ticket earlier, so its workgroup is running; wait for its
-    // ready flag (bounded: a lost flag gives a wrong tile, never a hung GPU)
-    if (threadIdx.x == 0) {
-      for (int j = 0; j < np; ++j) {
-        if (j == me) continue;
-        int* f = g.sk_flag + slot_of(s_first + j);
-        for (int spin = 0; spin < (1 << 24) && __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0;
-             ++spin)
-          __builtin_amdgcn_s_sleep(2);
-      }
-    }
-    __syncthreads();
-    // k order ((p0 + p1) + p2) with at most three pieces (the launcher keeps every workgroup's range
-    // at least half a tile long): a two-term sum is exact in either order, so only the third piece,
-    // when it is this one, needs the first two summed apart
-    const int oa = me == 0 ? 1 : 0;                    // first other piece
-    const int ob = np == 3 ? (me == 2 ? 1 : 2) : -1;  // second other piece (or none)
-    const uint32_t base_a = (uint32_t)slot_of(s_first + oa) * (SK_SLOT_FLOATS * 4) + tid16;
-    const uint32_t base_b = (uint32_t)slot_of(s_first + (ob >= 0 ? ob : oa)) * (SK_SLOT_FLOATS * 4) + tid16;
-    const bool three = ob >= 0, last_piece = me == 2;
-    auto ld = [&](uint32_t base, int r) -> f32x4 {
-      return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(part, base, r * (G8_THREADS * 16), 16));
-    };
-    const int tm = T / tiles_n;
-    const int m0 = tm * BM, n0 = (T - tm * tiles_n) * BN;
-    constexpr int SPB = (EPI == EPI_F32_RESIDUAL || EPI == EPI_F32) ? 2 : 1;
-    // the tile's epilogue, one (h, hh, i) block pair at a time, from the summed pieces
-    static_for<2>([&](auto hh_c) {
-      constexpr int hh = decltype(hh_c)::value;
-      const int n = n0 + WN * wc + HN * hh + 8 * fq;
-      float bn[8];
-#pragma unroll
-      for (int r = 0; r < 8; ++r) bn[r] = sbias[n + r];
-      static_for<2>([&](auto h_c) {
-        constexpr int h = decltype(h_c)::value;
-        static_for<NI>([&](auto i_c) {
-          constexpr int i = decltype(i_c)::value;
-          constexpr int r0 = ((h * 2 + hh) * NI + i) * NJ;
-          f32x4 v[NJ];
-#pragma unroll
-          for (int jb = 0; jb < NJ; ++jb) {
-            const f32x4 xa = ld(base_a, r0 + jb);
-            const f32x4 xb = three ? ld(base_b, r0 + jb) : f32x4{};
-            const f32x4 a = acc[h][hh][i][jb];
-            v[jb] = !three ? a + xa : (last_piece ? (xa + xb) + a : (a + xa) + xb);
-          }
-          const int mb = m0 + WM * wr + HM * h + 16 * i;
-          const int m = mb + fr;
-          if (mb < g.M) {
-            st_cnt += SPB;
-            if (m < g.M) gemm_store8<EPI>(g, m, n, v[0], v[1], bn);
-          }
-        });
-      });
-    });
-    if (threadIdx.x == 0) {  // every piece has arrived and handed over: reset for the next launch
-      for (int j = 0; j < np; ++j)
-        if (j != me) __hip_atomic_store(g.sk_flag + slot_of(s_first + j), 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(g.sk_cnt + T, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  };
-
   // waves 4..7 (one per SIMD beside a wave of 0..3) run one barrier behind waves 0..3
   if (wr == 1) bar();
   int phi = 0;
@@ -669,11 +584,6 @@ __global__ __launch_bounds__(G8_THREADS) void gemm_8p_kernel(GemmArgs g) {
     }
     st_phi = phi - 1;
     st_cnt = 0;
-    if (SK && (kb != 0 || ke != ktiles)) {  // wave-uniform: a cut tile
-      sk_handoff(T - lo, T);
-      if (wr == 1) bar();  // restore the stagger (equal barrier counts in both groups)
-      continue;
-    }
 
     // epilogue: blocks (h, hh, i): row WM wr + HM h + 16 i + fr; columns WN wc + HN hh + 8 fq
     // + (0..7) from the block pair jb = 0, 1 (one 16-byte f16 store, two for f32)
@@ -686,6 +596,19 @@ __global__ __launch_bounds__(G8_THREADS) void gemm_8p_kernel(GemmArgs g) {
       float bn[8];
 #pragma unroll
       for (int r = 0; r < 8; ++r) bn[r] = sbias[n + r];
+      // residual: the half's old C values in one batch of loads (rows clamped into the matrix)
+      f32x4 cv[2][NI][2];
+      if constexpr (EPI == EPI_F32_RESIDUAL) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int i = 0; i < NI; ++i) {
+            const int mc = min(m0 + WM * wr + HM * h + 16 * i + fr, g.M - 1);
+            const f32x4* p = (const f32x4*)((const float*)g.C + (size_t)mc * g.ldc + n);
+            cv[h][i][0] = p[0];
+            cv[h][i][1] = p[1];
+          }
+      }
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
 #pragma unroll
@@ -694,7 +617,12 @@ __global__ __launch_bounds__(G8_THREADS) void gemm_8p_kernel(GemmArgs g) {
           const int m = mb + fr;
           if (mb < g.M) {  // uniform branch: a block with a valid row issues exactly
             st_cnt += SPB;  // SPB vector stores (counted for the vmcnt bookkeeping)
-            if (m < g.M) gemm_store8<EPI>(g, m, n, acc[h][hh][i][0], acc[h][hh][i][1], bn);
+            if (m < g.M) {
+              if constexpr (EPI == EPI_F32_RESIDUAL)
+                gemm_store8_res(g, m, n, acc[h][hh][i][0], acc[h][hh][i][1], bn, cv[h][i][0], cv[h][i][1]);
+              else
+                gemm_store8<EPI>(g, m, n, acc[h][hh][i][0], acc[h][hh][i][1], bn);
+            }
           }
         }
       }
@@ -1333,71 +1261,8 @@ int launch_epi(int epi, dim3 grid, dim3 block, hipStream_t s, const GemmArgs& g)
 }
 template <int EPI>
 struct K3dKern {
-  static constexpr auto fn = gemm_8p_kernel<EPI, 0>;
+  static constexpr auto fn = gemm_8p_kernel<EPI>;
 };
-template <int EPI>
-struct K3dSkKern {
-  static constexpr auto fn = gemm_8p_kernel<EPI, 1>;
-};
-
-// K3d stream-K (SK) for the image tower's batches (lib_ok calls, M >= 4096): where the
-// data-parallel tile rounds leave CUs idle. Estimated in K-tile steps per CU: DP =
-// ceil(tiles / CUs) * k-tiles; SK = tiles * k-tiles / CUs + 3 steps for the cut tiles' hand-off
-// (a 256 KiB partial stored or read). ViT-B/32 at B = 256: out-proj / fc2 / patch embed (150
-// tiles) and fc1 (600) take SK, qkv (450) stays data-parallel. The text towers never take it: a
-// query row there must not depend on its batch (retrieve_batch == retrieve, bit for bit).
-bool g8_use_sk(const GemmArgs& g, int ntiles, int cus) {
-  if (!g.lib_ok || g.M < 4096) return false;
-  const double kt = g.K / GK;
-  // every workgroup's range at least half a tile (so a tile has at most three pieces: the
-  // kernel's k-order sum) and at least two K-tiles; per XCD: ntiles / 8 tiles over cus / 8 groups
-  const int kti = g.K / GK;
-  const int lmin = (ntiles / 8) * kti / (cus / 8);
-  if (lmin < std::max(2, (kti + 1) / 2)) return false;
-  const double dp = (double)((ntiles + cus - 1) / cus) * kt;
-  const double sk = (double)ntiles * kt / cus + 3.0;
-  return sk < 0.9 * dp;
-}
-
-// Per-(device, stream) SK workspace: two partial slots per workgroup, a ticket per tile and a flag
-// per slot, zeroed once (every launch leaves them zero). Launches on one stream are ordered and
-// share it; concurrent streams get their own.
-struct SkWorkspace {
-  float* part = nullptr;
-  int* cnt = nullptr;
-  int* flag = nullptr;
-  int slots = 0, counters = 0;
-};
-
-int sk_workspace(hipStream_t s, int grid, int ntiles, GemmArgs& g) {
-  static std::mutex mu;
-  static std::map<std::pair<int, hipStream_t>, SkWorkspace> pool;
-  int dev = 0;
-  MRAG_HIP(hipGetDevice(&dev));
-  std::lock_guard<std::mutex> lk(mu);
-  SkWorkspace& w = pool[{dev, s}];
-  if (w.slots < 2 * grid || w.counters < ntiles) {
-    if (w.part) {  // the stream's earlier launches may still use the old buffers
-      MRAG_HIP(hipStreamSynchronize(s));
-      (void)hipFree(w.part);
-      (void)hipFree(w.cnt);
-      (void)hipFree(w.flag);
-      w = SkWorkspace{};
-    }
-    const int slots = 2 * std::max(grid, 256), counters = std::max(ntiles, 4096);
-    MRAG_HIP(hipMalloc(&w.part, (size_t)slots * SK_SLOT_FLOATS * 4));
-    MRAG_HIP(hipMalloc(&w.cnt, (size_t)counters * 4));
-    MRAG_HIP(hipMalloc(&w.flag, (size_t)slots * 4));
-    MRAG_HIP(hipMemsetAsync(w.cnt, 0, (size_t)counters * 4, s));
-    MRAG_HIP(hipMemsetAsync(w.flag, 0, (size_t)slots * 4, s));
-    w.slots = slots;
-    w.counters = counters;
-  }
-  g.sk_part = w.part;
-  g.sk_cnt = w.cnt;
-  g.sk_flag = w.flag;
-  return MRAG_OK;
-}
 template <int EPI>
 struct K3Kern {
   static constexpr auto fn = gemm_nt_kernel<EPI>;
@@ -1408,22 +1273,10 @@ int launch_gemm(const GemmArgs& g, int epi, hipStream_t s) {
   MRAG_REQUIRE(g.N % GN == 0 && g.K % GK == 0, "gemm: N=%d must be a multiple of %d and K=%d of %d", g.N, GN, g.K,
                GK);
   MRAG_REQUIRE(g.lda % 8 == 0 && g.ldw % 8 == 0 && g.ldc % 4 == 0, "gemm: lda/ldw must be multiples of 8, ldc of 4");
-  const bool lib_only = epi == EPI_F16_SWISH_LIB || (g.alpha != 0.f && g.alpha != 1.f);
-  if (blaslt_eligible(g, epi)) {
-    const int rc = launch_gemm_blaslt(g, epi, s);
-    if (rc != MRAG_ERR_UNSUPPORTED || lib_only) return rc;
-  } else if (lib_only) {
-    return MRAG_ERR_UNSUPPORTED;  // no hand-written form: the caller takes its K3 / K3d path
-  }
+  MRAG_REQUIRE(((uintptr_t)g.bias & 15) == 0 && ((uintptr_t)g.C & 15) == 0, "gemm: bias and C must be 16-byte aligned");
   if (g.M >= 1024 && g.N <= G8_BIAS_MAX && g.N % 256 == 0 && !k3_beats_k3d(g)) {
     const int ntiles = ((g.M + G8Geom::BM - 1) / G8Geom::BM) * (g.N / G8Geom::BN);
-    const int cus = std::max(8, num_cus() / 8 * 8);
-    if (g8_use_sk(g, ntiles, cus)) {
-      GemmArgs gs = g;
-      if (int rc = sk_workspace(s, cus, ntiles, gs)) return rc;
-      return launch_epi<K3dSkKern>(epi, dim3((unsigned)cus), dim3(G8_THREADS), s, gs);
-    }
-    const int nb = std::min((ntiles + 7) / 8 * 8, cus);
+    const int nb = std::min((ntiles + 7) / 8 * 8, std::max(8, num_cus() / 8 * 8));
     return launch_epi<K3dKern>(epi, dim3((unsigned)nb), dim3(G8_THREADS), s, g);
   }
   const dim3 grid((unsigned)(((g.M + GM - 1) / GM) * (g.N / GN)));
