@@ -17,7 +17,6 @@ from app.encoders import gemm_nt  # noqa: E402
 SHAPES = {  # name: (M, N, K, epilogue)
     "qkv": (12800, 2304, 768, 0),
     "fc1": (12800, 3072, 768, 1),
-    "fc1s": (12800, 3072, 768, 5),  # the library's swish form (image tower on hipBLASLt)
     "fc2": (12800, 768, 3072, 3),
     "out": (12800, 768, 768, 3),
     "sq4k": (4096, 4096, 4096, 0),

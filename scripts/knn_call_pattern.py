@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """The bench's call-pattern leg alone (one query per search over 1M x 512, bench.call_pattern_leg):
-prints one JSON line. env MRAG_SCAN_SMALLQ=0 runs small batches on the 256-query scan (A/B)."""
+prints one JSON line."""
 import json
 import os
 import sys
@@ -22,5 +22,4 @@ ix.add(x)
 del x
 q = torch.randn((bench.NQ, bench.DIM), generator=torch.Generator(device=dev).manual_seed(1), device=dev)
 out = bench.call_pattern_leg(ix, q, reps=int(os.environ.get("REPS", "200")))
-out["env_smallq"] = os.environ.get("MRAG_SCAN_SMALLQ")
 print(json.dumps(out), flush=True)

@@ -37,5 +37,4 @@ for dim in (384, 512):
             ms, n = ix.profile(0)
             unc, _ = ix.last_stats()
         print(json.dumps({"dim": dim, "rows": 1 << 19, "k": k, "scan_ms": round(ms / n, 4),
-                          "search_ms": round(e0.elapsed_time(e1) / 10, 4), "uncertified": unc,
-                          "stride_bigk": os.environ.get("MRAG_K7_STRIDE_BIGK", "16")}), flush=True)
+                          "search_ms": round(e0.elapsed_time(e1) / 10, 4), "uncertified": unc}), flush=True)
