@@ -46,9 +46,6 @@ void buf_free(Buf& b) {
 
 struct Layer {
   Buf wqkv, bqkv, wo, bo, w1, b1, w2, b2, ln1g, ln1b, ln2g, ln2b;
-  // the LayerNorm feeding q|k|v / fc1 folded into them (EPI_FOLD): f16 W diag(gamma), bias + W beta,
-  // column sums of the folded weight; built from the uploaded parameters before the first forward
-  Buf wqkv_f, bqkv_f, cqkv, w1_f, b1_f, c1;
 };
 
 __global__ void f32_to_f16_kernel(const float* __restrict__ in, _Float16* __restrict__ out, int64_t n) {
@@ -73,10 +70,6 @@ struct mrag_encoder {
   // workspace
   Buf X, H16, QKV, ATT, F16, PATCH, IMG, IDS, MASK, TYPES, ROWS, POOL16, OUT;
   Buf XG, AG, HG, FG;  // the pooled rows of a CLIP tower's last layer (clip_layer_pooled)
-  // LayerNorm row statistics (EPI_STATS partials, [rows][D / 64] float2): ST0 / ST1 per token,
-  // STG for the pooled rows
-  Buf ST0, ST1, STG;
-  bool folded = false;  // the Layer::*_f buffers match the uploaded parameters
   int64_t ws_tokens = 0, ws_batch = 0;
   // Device-pointer calls return without a host sync (stream-ordered, like any kernel launch):
   // `done` marks the end of the last call's work on `last_stream`; a call on another stream
@@ -244,7 +237,6 @@ int ensure_workspace(mrag_encoder* e, int B, int T) {
     if (int rc = buf_ensure(e->FG, (size_t)B * I * 2)) return rc;
     if (int rc = buf_ensure(e->ROWS, (size_t)B * 4 + 256)) return rc;
     if (int rc = buf_ensure(e->POOL16, (size_t)B * D * 2)) return rc;
-    if (int rc = buf_ensure(e->STG, (size_t)B * (D / 64) * 8)) return rc;
     if (c.kind == MRAG_ENC_BERT_PAIR)
       if (int rc = buf_ensure(e->POOL32, (size_t)B * D * 4)) return rc;
     e->ws_batch = B;
@@ -254,8 +246,6 @@ int ensure_workspace(mrag_encoder* e, int B, int T) {
   if (int rc = buf_ensure(e->H16, tokens * D * 2)) return rc;
   if (int rc = buf_ensure(e->QKV, tokens * 3 * D * 2)) return rc;
   if (int rc = buf_ensure(e->ATT, tokens * D * 2)) return rc;
-  if (int rc = buf_ensure(e->ST0, tokens * (D / 64) * 8)) return rc;
-  if (int rc = buf_ensure(e->ST1, tokens * (D / 64) * 8)) return rc;
   int64_t f16n = tokens * I;
   if (c.kind == MRAG_ENC_CLIP_VISION) f16n = std::max<int64_t>(f16n, tokens * 3 * c.patch_size * c.patch_size);
   if (int rc = buf_ensure(e->F16, f16n * 2)) return rc;
@@ -283,74 +273,6 @@ int gemm(const void* A, const void* W, const void* bias, void* C, int M, int N, 
   return launch_gemm(g, epi, s);
 }
 
-GemmArgs gargs(const void* A, const void* W, const void* bias, void* C, int M, int N, int K, int ldc) {
-  GemmArgs g{};
-  g.A = (const _Float16*)A;
-  g.W = (const _Float16*)W;
-  g.bias = (const float*)bias;
-  g.C = C;
-  g.M = M;
-  g.N = N;
-  g.K = K;
-  g.lda = K;
-  g.ldw = K;
-  g.ldc = ldc;
-  return g;
-}
-
-// EPI_FOLD / EPI_RESLN inputs: row partials st (p per row) of a LayerNorm over D
-GemmArgs& ln_in(GemmArgs& g, const void* st, int p, int D, float eps) {
-  g.st_in = (const float2*)st;
-  g.st_in_p = p;
-  g.ln_d = D;
-  g.ln_eps = eps;
-  return g;
-}
-
-// EPI_STATS outputs: the f16 copy of the new residual and its row partials
-GemmArgs& stats_out(GemmArgs& g, void* c16, void* st) {
-  g.c16 = (_Float16*)c16;
-  g.st_out = (float2*)st;
-  return g;
-}
-
-// Fold every LayerNorm that feeds a GEMM into that GEMM's weights (EPI_FOLD): CLIP (pre-LN):
-// q|k|v <- layer_norm1, fc1 <- layer_norm2 of the same layer; BERT (post-LN): q|k|v of layer
-// l >= 1 <- output.LayerNorm of layer l - 1, intermediate.dense <- attention.output.LayerNorm.
-int prepare_folds(mrag_encoder* e) {
-  if (e->folded) return MRAG_OK;
-  const auto& c = e->cfg;
-  const int D = c.hidden, I = c.intermediate;
-  const bool bert = c.kind == MRAG_ENC_BERT || c.kind == MRAG_ENC_BERT_PAIR;
-  hipStream_t s = e->stream;
-  for (int l = 0; l < c.layers; ++l) {
-    Layer& L = e->layers[l];
-    const Buf* qg = bert ? (l > 0 ? &e->layers[l - 1].ln2g : nullptr) : &L.ln1g;
-    const Buf* qb = bert ? (l > 0 ? &e->layers[l - 1].ln2b : nullptr) : &L.ln1b;
-    const Buf& fg = bert ? L.ln1g : L.ln2g;
-    const Buf& fb = bert ? L.ln1b : L.ln2b;
-    if (qg) {
-      if (int rc = buf_ensure(L.wqkv_f, (size_t)3 * D * D * 2)) return rc;
-      if (int rc = buf_ensure(L.bqkv_f, (size_t)3 * D * 4)) return rc;
-      if (int rc = buf_ensure(L.cqkv, (size_t)3 * D * 4)) return rc;
-      if (int rc = launch_ln_fold_weight((const _Float16*)L.wqkv.p, (const float*)qg->p, (const float*)qb->p,
-                                         (const float*)L.bqkv.p, 3 * D, D, (_Float16*)L.wqkv_f.p, (float*)L.bqkv_f.p,
-                                         (float*)L.cqkv.p, s))
-        return rc;
-    }
-    if (int rc = buf_ensure(L.w1_f, (size_t)I * D * 2)) return rc;
-    if (int rc = buf_ensure(L.b1_f, (size_t)I * 4)) return rc;
-    if (int rc = buf_ensure(L.c1, (size_t)I * 4)) return rc;
-    if (int rc = launch_ln_fold_weight((const _Float16*)L.w1.p, (const float*)fg.p, (const float*)fb.p,
-                                       (const float*)L.b1.p, I, D, (_Float16*)L.w1_f.p, (float*)L.b1_f.p,
-                                       (float*)L.c1.p, s))
-      return rc;
-  }
-  MRAG_HIP(hipStreamSynchronize(s));
-  e->folded = true;
-  return MRAG_OK;
-}
-
 int layernorm(const float* x, const int* gather, float* y32, _Float16* y16, const Buf& g, const Buf& b, int rows,
               int D, float eps, hipStream_t s) {
   LayerNormArgs a{};
@@ -367,26 +289,14 @@ int layernorm(const float* x, const int* gather, float* y32, _Float16* y16, cons
   return launch_layernorm(a, s);
 }
 
-// q|k|v of a CLIP layer from the raw residual stream: LN1 folded (EPI_FOLD) with the row
-// partials of X in ST0 (st_p per row: 1 after the embeddings, D / 64 after a residual GEMM)
-int clip_qkv(mrag_encoder* e, const Layer& L, int M, int st_p, hipStream_t s) {
-  const auto& c = e->cfg;
-  const int D = c.hidden;
-  GemmArgs q = gargs(e->H16.p, L.wqkv_f.p, L.bqkv_f.p, e->QKV.p, M, 3 * D, D, 3 * D);
-  ln_in(q, e->ST0.p, st_p, D, c.ln_eps).colsum = (const float*)L.cqkv.p;
-  return launch_gemm(q, EPI_F16 | EPI_FOLD, s);
-}
-
-// Pre-LN transformer layer (CLIP): X += attn(LN1(X)); X += mlp(LN2(X)). Both LayerNorms are
-// folded into the GEMMs they feed: on entry and exit X (f32), H16 = f16(X) and ST0 = X's row
-// partials (st_p per row on entry, D / 64 on exit), written by the residual GEMMs' epilogues.
-int clip_layer(mrag_encoder* e, const Layer& L, int B, int T, const int32_t* mask, int causal, int st_p,
-               hipStream_t s) {
+// Pre-LN transformer layer (CLIP): X += attn(LN1(X)); X += mlp(LN2(X)).
+int clip_layer(mrag_encoder* e, const Layer& L, int B, int T, const int32_t* mask, int causal, hipStream_t s) {
   const auto& c = e->cfg;
   const int D = c.hidden, I = c.intermediate, M = B * T;
   float* X = (float*)e->X.p;
   _Float16* H = (_Float16*)e->H16.p;
-  if (int rc = clip_qkv(e, L, M, st_p, s)) return rc;
+  if (int rc = layernorm(X, nullptr, nullptr, H, L.ln1g, L.ln1b, M, D, c.ln_eps, s)) return rc;
+  if (int rc = gemm(H, L.wqkv.p, L.bqkv.p, e->QKV.p, M, 3 * D, D, 3 * D, EPI_F16, s)) return rc;
   AttentionArgs a{};
   a.qkv = (const _Float16*)e->QKV.p;
   a.out = (_Float16*)e->ATT.p;
@@ -397,14 +307,11 @@ int clip_layer(mrag_encoder* e, const Layer& L, int B, int T, const int32_t* mas
   a.causal = causal;
   a.scale = 1.0f / sqrtf((float)(D / c.heads));
   if (int rc = launch_attention(a, D / c.heads, s)) return rc;
-  GemmArgs o = gargs(e->ATT.p, L.wo.p, L.bo.p, X, M, D, D, D);
-  if (int rc = launch_gemm(stats_out(o, H, e->ST0.p), EPI_F32_RESIDUAL | EPI_STATS, s)) return rc;
+  if (int rc = gemm(e->ATT.p, L.wo.p, L.bo.p, X, M, D, D, D, EPI_F32_RESIDUAL, s)) return rc;
+  if (int rc = layernorm(X, nullptr, nullptr, H, L.ln2g, L.ln2b, M, D, c.ln_eps, s)) return rc;
   const int act = c.act == 0 ? EPI_F16_QUICK_GELU : EPI_F16_GELU_ERF;
-  GemmArgs f1 = gargs(H, L.w1_f.p, L.b1_f.p, e->F16.p, M, I, D, I);
-  ln_in(f1, e->ST0.p, D / 64, D, c.ln_eps).colsum = (const float*)L.c1.p;
-  if (int rc = launch_gemm(f1, act | EPI_FOLD, s)) return rc;
-  GemmArgs f2 = gargs(e->F16.p, L.w2.p, L.b2.p, X, M, D, I, D);
-  return launch_gemm(stats_out(f2, H, e->ST0.p), EPI_F32_RESIDUAL | EPI_STATS, s);
+  if (int rc = gemm(H, L.w1.p, L.b1.p, e->F16.p, M, I, D, I, act, s)) return rc;
+  return gemm(e->F16.p, L.w2.p, L.b2.p, X, M, D, I, D, EPI_F32_RESIDUAL, s);
 }
 
 // The LAST pre-LN layer of a tower that pools one row per sequence (CLIP: the class token of
@@ -416,11 +323,13 @@ int clip_layer(mrag_encoder* e, const Layer& L, int B, int T, const int32_t* mas
 // (A/B check against the full layer in scripts/enc_dump.py). ViT-B/32 at
 // B = 256: the layer's out-proj / fc1 / fc2 run on 256 rows instead of 12,800.
 int clip_layer_pooled(mrag_encoder* e, const Layer& L, int B, int T, const int32_t* mask, int causal, const int* rows,
-                      int st_p, hipStream_t s) {
+                      hipStream_t s) {
   const auto& c = e->cfg;
   const int D = c.hidden, I = c.intermediate, M = B * T;
   float* X = (float*)e->X.p;
-  if (int rc = clip_qkv(e, L, M, st_p, s)) return rc;
+  _Float16* H = (_Float16*)e->H16.p;
+  if (int rc = layernorm(X, nullptr, nullptr, H, L.ln1g, L.ln1b, M, D, c.ln_eps, s)) return rc;
+  if (int rc = gemm(H, L.wqkv.p, L.bqkv.p, e->QKV.p, M, 3 * D, D, 3 * D, EPI_F16, s)) return rc;
   AttentionArgs a{};
   a.qkv = (const _Float16*)e->QKV.p;
   a.out = (_Float16*)e->ATT.p;
@@ -434,35 +343,21 @@ int clip_layer_pooled(mrag_encoder* e, const Layer& L, int B, int T, const int32
   if (int rc = launch_gather_rows(X, e->XG.p, rows, B, D * 4, s)) return rc;
   if (int rc = launch_gather_rows(e->ATT.p, e->AG.p, rows, B, D * 2, s)) return rc;
   float* XG = (float*)e->XG.p;
-  GemmArgs o = gargs(e->AG.p, L.wo.p, L.bo.p, XG, B, D, D, D);
-  if (int rc = launch_gemm(stats_out(o, e->HG.p, e->STG.p), EPI_F32_RESIDUAL | EPI_STATS, s)) return rc;
+  if (int rc = gemm(e->AG.p, L.wo.p, L.bo.p, XG, B, D, D, D, EPI_F32_RESIDUAL, s)) return rc;
+  if (int rc = layernorm(XG, nullptr, nullptr, (_Float16*)e->HG.p, L.ln2g, L.ln2b, B, D, c.ln_eps, s)) return rc;
   const int act = c.act == 0 ? EPI_F16_QUICK_GELU : EPI_F16_GELU_ERF;
-  GemmArgs f1 = gargs(e->HG.p, L.w1_f.p, L.b1_f.p, e->FG.p, B, I, D, I);
-  ln_in(f1, e->STG.p, D / 64, D, c.ln_eps).colsum = (const float*)L.c1.p;
-  if (int rc = launch_gemm(f1, act | EPI_FOLD, s)) return rc;
+  if (int rc = gemm(e->HG.p, L.w1.p, L.b1.p, e->FG.p, B, I, D, I, act, s)) return rc;
   return gemm(e->FG.p, L.w2.p, L.b2.p, XG, B, D, I, D, EPI_F32_RESIDUAL, s);
 }
 
-// Post-LN transformer layer (BERT): X = LN1(X + attn(X)); X = LN2(X + ffn(X)), with both
-// LayerNorms folded: the GEMMs after a LayerNorm read the raw sum (EPI_FOLD), and the residual
-// GEMM that adds to a normalised row normalises the old row in its epilogue (EPI_RESLN).
-// Layer 0 enters with X = the embedding LayerNorm's output and H16 = f16(X); layer l > 0 with
-// X = the previous layer's raw sum y2 (its LN2 not applied), H16 = f16(y2), ST0 = y2's row
-// partials. On exit X = y2, H16 = f16(y2), ST0 = its partials (ST1 holds the LN1 input's).
-int bert_layer(mrag_encoder* e, int l, int B, int T, const int32_t* mask, hipStream_t s) {
+// Post-LN transformer layer (BERT): X = LN(X + attn(X)); X = LN(X + ffn(X)).
+// Invariant on entry and exit: X (f32) and H16 == f16(X).
+int bert_layer(mrag_encoder* e, const Layer& L, int B, int T, const int32_t* mask, hipStream_t s) {
   const auto& c = e->cfg;
-  const Layer& L = e->layers[l];
-  const int D = c.hidden, I = c.intermediate, M = B * T, P = D / 64;
+  const int D = c.hidden, I = c.intermediate, M = B * T;
   float* X = (float*)e->X.p;
   _Float16* H = (_Float16*)e->H16.p;
-  const Layer* prev = l > 0 ? &e->layers[l - 1] : nullptr;
-  if (!prev) {
-    if (int rc = gemm(H, L.wqkv.p, L.bqkv.p, e->QKV.p, M, 3 * D, D, 3 * D, EPI_F16, s)) return rc;
-  } else {
-    GemmArgs q = gargs(H, L.wqkv_f.p, L.bqkv_f.p, e->QKV.p, M, 3 * D, D, 3 * D);
-    ln_in(q, e->ST0.p, P, D, c.ln_eps).colsum = (const float*)L.cqkv.p;
-    if (int rc = launch_gemm(q, EPI_F16 | EPI_FOLD, s)) return rc;
-  }
+  if (int rc = gemm(H, L.wqkv.p, L.bqkv.p, e->QKV.p, M, 3 * D, D, 3 * D, EPI_F16, s)) return rc;
   AttentionArgs a{};
   a.qkv = (const _Float16*)e->QKV.p;
   a.out = (_Float16*)e->ATT.p;
@@ -473,41 +368,17 @@ int bert_layer(mrag_encoder* e, int l, int B, int T, const int32_t* mask, hipStr
   a.causal = 0;
   a.scale = 1.0f / sqrtf((float)(D / c.heads));
   if (int rc = launch_attention(a, D / c.heads, s)) return rc;
-  // y1 = LN2_prev(X) + attn . Wo + bo (layer 0: X is already normalised) -> X, H16, ST1
-  GemmArgs o = gargs(e->ATT.p, L.wo.p, L.bo.p, X, M, D, D, D);
-  stats_out(o, H, e->ST1.p);
-  if (prev) {
-    ln_in(o, e->ST0.p, P, D, c.ln_eps);
-    o.ln_g = (const float*)prev->ln2g.p;
-    o.ln_b = (const float*)prev->ln2b.p;
-  }
-  if (int rc = launch_gemm(o, EPI_F32_RESIDUAL | EPI_STATS | (prev ? EPI_RESLN : 0), s)) return rc;
-  GemmArgs f1 = gargs(H, L.w1_f.p, L.b1_f.p, e->F16.p, M, I, D, I);
-  ln_in(f1, e->ST1.p, P, D, c.ln_eps).colsum = (const float*)L.c1.p;
-  if (int rc = launch_gemm(f1, EPI_F16_GELU_ERF | EPI_FOLD, s)) return rc;
-  // y2 = LN1(y1) + ffn . W2 + b2 -> X, H16, ST0
-  GemmArgs f2 = gargs(e->F16.p, L.w2.p, L.b2.p, X, M, D, I, D);
-  stats_out(f2, H, e->ST0.p);
-  ln_in(f2, e->ST1.p, P, D, c.ln_eps);
-  f2.ln_g = (const float*)L.ln1g.p;
-  f2.ln_b = (const float*)L.ln1b.p;
-  return launch_gemm(f2, EPI_F32_RESIDUAL | EPI_STATS | EPI_RESLN, s);
-}
-
-// BERT layers, then the last layer's output LayerNorm (X normalised in place, H16 = f16(X)).
-int bert_layers(mrag_encoder* e, int B, int T, const int32_t* mask, hipStream_t s) {
-  const auto& c = e->cfg;
-  for (int l = 0; l < c.layers; ++l)
-    if (int rc = bert_layer(e, l, B, T, mask, s)) return rc;
-  float* X = (float*)e->X.p;
-  const Layer& last = e->layers[c.layers - 1];
-  return layernorm(X, nullptr, X, (_Float16*)e->H16.p, last.ln2g, last.ln2b, B * T, c.hidden, c.ln_eps, s);
+  if (int rc = gemm(e->ATT.p, L.wo.p, L.bo.p, X, M, D, D, D, EPI_F32_RESIDUAL, s)) return rc;
+  if (int rc = layernorm(X, nullptr, X, H, L.ln1g, L.ln1b, M, D, c.ln_eps, s)) return rc;
+  if (int rc = gemm(H, L.w1.p, L.b1.p, e->F16.p, M, I, D, I, EPI_F16_GELU_ERF, s)) return rc;
+  if (int rc = gemm(e->F16.p, L.w2.p, L.b2.p, X, M, D, I, D, EPI_F32_RESIDUAL, s)) return rc;
+  return layernorm(X, nullptr, X, H, L.ln2g, L.ln2b, M, D, c.ln_eps, s);
 }
 
 int check_ready(mrag_encoder* e) {
   for (const auto& n : e->expected)
     if (!e->loaded.count(n)) return mrag::fail(MRAG_ERR_STATE, "encoder parameter '%s' not set", n.c_str());
-  return prepare_folds(e);
+  return MRAG_OK;
 }
 
 }  // namespace
@@ -565,13 +436,12 @@ int mrag_encoder_destroy(mrag_encoder* e) {
     if (e->done) (void)hipEventDestroy(e->done);
     if (e->null_ev) (void)hipEventDestroy(e->null_ev);
     for (auto& L : e->layers)
-      for (Buf* b : {&L.wqkv, &L.bqkv, &L.wo, &L.bo, &L.w1, &L.b1, &L.w2, &L.b2, &L.ln1g, &L.ln1b, &L.ln2g, &L.ln2b,
-                     &L.wqkv_f, &L.bqkv_f, &L.cqkv, &L.w1_f, &L.b1_f, &L.c1})
+      for (Buf* b : {&L.wqkv, &L.bqkv, &L.wo, &L.bo, &L.w1, &L.b1, &L.w2, &L.b2, &L.ln1g, &L.ln1b, &L.ln2g, &L.ln2b})
         buf_free(*b);
     for (Buf* b : {&e->patch_w, &e->cls, &e->pos, &e->pre_g, &e->pre_b, &e->post_g, &e->post_b, &e->proj_w, &e->tok,
                    &e->type0, &e->emb_g, &e->emb_b, &e->X, &e->H16, &e->QKV, &e->ATT, &e->F16, &e->PATCH, &e->IMG,
                    &e->IDS, &e->MASK, &e->ROWS, &e->POOL16, &e->OUT, &e->pool_w, &e->pool_b, &e->cls_w, &e->cls_b,
-                   &e->POOL32, &e->TYPES, &e->XG, &e->AG, &e->HG, &e->FG, &e->ST0, &e->ST1, &e->STG})
+                   &e->POOL32, &e->TYPES, &e->XG, &e->AG, &e->HG, &e->FG})
       buf_free(*b);
     (void)hipStreamDestroy(e->stream);
   }
@@ -664,7 +534,6 @@ int mrag_encoder_set_param(mrag_encoder* e, const char* cname, const float* data
   if (rc) return rc;
   MRAG_HIP(hipStreamSynchronize(s));
   e->loaded[name] = true;
-  e->folded = false;
   return MRAG_OK;
 }
 
@@ -724,16 +593,14 @@ int mrag_encoder_embed_images(mrag_encoder* e, const uint8_t* images, int32_t ba
   if (int rc = launch_vit_im2col(img, (_Float16*)e->F16.p, B, S, P, s)) return rc;
   if (int rc = gemm(e->F16.p, e->patch_w.p, nullptr, e->PATCH.p, B * (T - 1), D, Kp, D, EPI_F32, s)) return rc;
   if (int rc = launch_vit_embed_ln((const float*)e->PATCH.p, (const float*)e->cls.p, (const float*)e->pos.p,
-                                   (const float*)e->pre_g.p, (const float*)e->pre_b.p, X, (_Float16*)e->H16.p,
-                                   (float2*)e->ST0.p, B, T, D, c.ln_eps, s))
+                                   (const float*)e->pre_g.p, (const float*)e->pre_b.p, X, B, T, D, c.ln_eps, s))
     return rc;
   if (int rc = launch_cls_rows(B, T, (int*)e->ROWS.p, s)) return rc;
   const bool prune = c.layers > 0;
   for (int i = 0; i < c.layers; ++i) {
-    const int st_p = i == 0 ? 1 : D / 64;
     if (prune && i == c.layers - 1) {
-      if (int rc = clip_layer_pooled(e, e->layers[i], B, T, nullptr, 0, (const int*)e->ROWS.p, st_p, s)) return rc;
-    } else if (int rc = clip_layer(e, e->layers[i], B, T, nullptr, 0, st_p, s)) {
+      if (int rc = clip_layer_pooled(e, e->layers[i], B, T, nullptr, 0, (const int*)e->ROWS.p, s)) return rc;
+    } else if (int rc = clip_layer(e, e->layers[i], B, T, nullptr, 0, s)) {
       return rc;
     }
   }
@@ -794,16 +661,15 @@ int mrag_encoder_embed_tokens(mrag_encoder* e, const int32_t* ids, const int32_t
     dst = (float*)e->OUT.p;
   }
   if (c.kind == MRAG_ENC_CLIP_TEXT) {
-    if (int rc = launch_token_embed(dids, (const float*)e->tok.p, (const float*)e->pos.p, nullptr, nullptr, X, H,
-                                    (float2*)e->ST0.p, B, T, D, c.vocab, s))
+    if (int rc = launch_token_embed(dids, (const float*)e->tok.p, (const float*)e->pos.p, nullptr, nullptr, X, B, T, D,
+                                    c.vocab, s))
       return rc;
     if (int rc = launch_eos_rows(dids, B, T, c.eos_token_id, (int*)e->ROWS.p, s)) return rc;
     const bool prune = c.layers > 0;
     for (int i = 0; i < c.layers; ++i) {
-      const int st_p = i == 0 ? 1 : D / 64;
       if (prune && i == c.layers - 1) {
-        if (int rc = clip_layer_pooled(e, e->layers[i], B, T, dmask, 1, (const int*)e->ROWS.p, st_p, s)) return rc;
-      } else if (int rc = clip_layer(e, e->layers[i], B, T, dmask, 1, st_p, s)) {
+        if (int rc = clip_layer_pooled(e, e->layers[i], B, T, dmask, 1, (const int*)e->ROWS.p, s)) return rc;
+      } else if (int rc = clip_layer(e, e->layers[i], B, T, dmask, 1, s)) {
         return rc;
       }
     }
@@ -813,10 +679,11 @@ int mrag_encoder_embed_tokens(mrag_encoder* e, const int32_t* ids, const int32_t
     if (int rc = gemm(e->POOL16.p, e->proj_w.p, nullptr, dst, B, c.proj_dim, D, c.proj_dim, EPI_F32, s)) return rc;
   } else {
     if (int rc = launch_token_embed(dids, (const float*)e->tok.p, (const float*)e->pos.p, (const float*)e->type0.p,
-                                    nullptr, X, nullptr, nullptr, B, T, D, c.vocab, s))
+                                    nullptr, X, B, T, D, c.vocab, s))
       return rc;
     if (int rc = layernorm(X, nullptr, X, H, e->emb_g, e->emb_b, B * T, D, c.ln_eps, s)) return rc;
-    if (int rc = bert_layers(e, B, T, dmask, s)) return rc;
+    for (int i = 0; i < c.layers; ++i)
+      if (int rc = bert_layer(e, e->layers[i], B, T, dmask, s)) return rc;
     if (int rc = launch_mean_pool(X, dmask, dst, B, T, D, s)) return rc;
   }
   if (normalize)
@@ -866,10 +733,11 @@ int mrag_encoder_score_pairs(mrag_encoder* e, const int32_t* ids, const int32_t*
   float* X = (float*)e->X.p;
   _Float16* H = (_Float16*)e->H16.p;
   if (int rc = launch_token_embed(dids, (const float*)e->tok.p, (const float*)e->pos.p, (const float*)e->type0.p, dtypes,
-                                  X, nullptr, nullptr, B, T, D, c.vocab, s))
+                                  X, B, T, D, c.vocab, s))
     return rc;
   if (int rc = layernorm(X, nullptr, X, H, e->emb_g, e->emb_b, B * T, D, c.ln_eps, s)) return rc;
-  if (int rc = bert_layers(e, B, T, dmask, s)) return rc;
+  for (int i = 0; i < c.layers; ++i)
+    if (int rc = bert_layer(e, e->layers[i], B, T, dmask, s)) return rc;
   // pooler: dense over the [CLS] rows (token 0 of each sequence: A rows strided by T*D)
   GemmArgs pg{};
   pg.A = H;
@@ -904,24 +772,3 @@ int mrag_gemm_nt(const void* A, const void* W, const float* bias, void* C, int32
 }
 
 }  // extern "C"
-
-// Diagnostic export (not in include/mrag.h; tests and scripts only): one GEMM with the
-// LayerNorm-fold epilogues (EPI_FOLD / EPI_STATS / EPI_RESLN flags of encoder_kernels.h) on
-// device pointers, ldc = N.
-extern "C" __attribute__((visibility("default"))) int mrag_debug_gemm_ln(
-    const void* A, const void* W, const float* bias, void* C, int32_t M, int32_t N, int32_t K, int32_t epi,
-    const float* st_in, int32_t st_in_p, int32_t ln_d, float ln_eps, const float* colsum, const float* ln_g,
-    const float* ln_b, void* c16, float* st_out, void* stream) {
-  MRAG_REQUIRE(A && W && C, "NULL pointer");
-  GemmArgs g = gargs(A, W, bias, C, M, N, K, N);
-  g.st_in = (const float2*)st_in;
-  g.st_in_p = st_in_p;
-  g.ln_d = ln_d;
-  g.ln_eps = ln_eps;
-  g.colsum = colsum;
-  g.ln_g = ln_g;
-  g.ln_b = ln_b;
-  g.c16 = (_Float16*)c16;
-  g.st_out = (float2*)st_out;
-  return launch_gemm(g, epi, (hipStream_t)stream);
-}

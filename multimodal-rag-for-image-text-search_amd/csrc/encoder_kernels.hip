@@ -45,11 +45,11 @@ __device__ __forceinline__ void glds_x4(const void* gsrc, uint32_t lds_addr) {
 // result does not depend on which kernel its batch size selected.
 template <int EPI>
 __device__ __forceinline__ float gemm_act(float x) {
-  if constexpr (epi_base(EPI) == EPI_F16_QUICK_GELU) {
+  if constexpr (EPI == EPI_F16_QUICK_GELU) {
     // x * sigmoid(1.702 x) with hardware exp2 / rcp (~1 ulp each; the result is rounded to
     // fp16) instead of a full-precision divide
     return x * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.702f * 1.44269504088896341f * x));
-  } else if constexpr (epi_base(EPI) == EPI_F16_GELU_ERF) {
+  } else if constexpr (EPI == EPI_F16_GELU_ERF) {
     // erf by Abramowitz & Stegun 7.1.26 with hardware rcp / exp2: a fraction of the cost of the
     // libm erff in the epilogue. The erf error (<= 1.5e-7 absolute) gives a GELU error of at most
     // 0.5 |x| 1.5e-7 + rcp/exp2 ulps, i.e. an ABSOLUTE bound (~1e-6 at |x| = 8): below the fp16
@@ -66,9 +66,31 @@ __device__ __forceinline__ float gemm_act(float x) {
   }
 }
 
-// Eight consecutive outputs C[m][n .. n + 7] (both kernels: lane group f of a 16 x 16 block
-// pair owns 8 consecutive columns, see g8_colperm): one 16-byte store for the f16 epilogues,
-// two for the f32 ones.
+// Finish four consecutive outputs C[m][n .. n + 3] = epilogue(v + bias) (K3).
+template <int EPI>
+__device__ __forceinline__ void gemm_store4(const GemmArgs& g, int m, int n, f32x4 v, const float* bn) {
+  typedef _Float16 half4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+  for (int r = 0; r < 4; ++r) v[r] += bn[r];
+  const size_t o = (size_t)m * g.ldc + n;
+  if constexpr (EPI == EPI_F16 || EPI == EPI_F16_QUICK_GELU || EPI == EPI_F16_GELU_ERF) {
+    half4 h;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) h[r] = (_Float16)gemm_act<EPI>(v[r]);
+    *(half4*)((_Float16*)g.C + o) = h;
+  } else if constexpr (EPI == EPI_F32_RESIDUAL) {
+    f32x4* p = (f32x4*)((float*)g.C + o);
+    f32x4 c = *p;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) c[r] += v[r];
+    *p = c;
+  } else {
+    *(f32x4*)((float*)g.C + o) = v;
+  }
+}
+
+// Eight consecutive outputs C[m][n .. n + 7] (K3d): one 16-byte store for the f16
+// epilogues, two for the f32 ones — the same per-element arithmetic as gemm_store4.
 template <int EPI>
 __device__ __forceinline__ void gemm_store8(const GemmArgs& g, int m, int n, f32x4 v0, f32x4 v1, const float* bn) {
 #pragma unroll
@@ -77,7 +99,7 @@ __device__ __forceinline__ void gemm_store8(const GemmArgs& g, int m, int n, f32
     v1[r] += bn[4 + r];
   }
   const size_t o = (size_t)m * g.ldc + n;
-  if constexpr (epi_base(EPI) <= EPI_F16_GELU_ERF) {
+  if constexpr (EPI == EPI_F16 || EPI == EPI_F16_QUICK_GELU || EPI == EPI_F16_GELU_ERF) {
     half8 h;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -85,6 +107,16 @@ __device__ __forceinline__ void gemm_store8(const GemmArgs& g, int m, int n, f32
       h[4 + r] = (_Float16)gemm_act<EPI>(v1[r]);
     }
     *(half8*)((_Float16*)g.C + o) = h;
+  } else if constexpr (EPI == EPI_F32_RESIDUAL) {
+    f32x4* p = (f32x4*)((float*)g.C + o);
+    f32x4 c0 = p[0], c1 = p[1];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      c0[r] += v0[r];
+      c1[r] += v1[r];
+    }
+    p[0] = c0;
+    p[1] = c1;
   } else {
     f32x4* p = (f32x4*)((float*)g.C + o);
     p[0] = v0;
@@ -92,145 +124,22 @@ __device__ __forceinline__ void gemm_store8(const GemmArgs& g, int m, int n, f32
   }
 }
 
-// The LayerNorm-fold epilogues turn contraction off and fuse explicitly (fmaf): with contraction
-// left to the compiler, unrolled copies of one expression were compiled differently (fused in
-// one row block, v_pk_mul + v_pk_add in another), so identical rows got statistics an ulp apart
-// depending on their position in the tile (scripts/gemm_ln_check.py).
-// The f32 residual epilogue for eight outputs with the old C values already loaded (the
-// epilogues load a batch of C blocks before storing any: a store may alias a later load, so
-// loads issued block by block between the stores cost one memory round trip per block):
-// C = C' + (acc + bias), C' = C or, with EPI_RESLN, LN(C) = (C - mu) r gamma + beta (the
-// arithmetic of ln_row4p). With EPI_STATS also the f16 copy and the statistics of the eight new
-// values, (sum, M2 = sum of squared deviations from their mean, two-pass in registers), merged
-// into the lane's running (s1, s2) of its earlier eight (`first`: none yet) by Chan's formula.
-template <int EPI>
+// gemm_store8 for the f32 residual epilogue with the old C values already loaded (the epilogues
+// load a batch of C blocks before storing any: a store may alias a later load, so loads issued
+// block by block between the stores cost one memory round trip per block). Same arithmetic:
+// C = C + (acc + bias).
 __device__ __forceinline__ void gemm_store8_res(const GemmArgs& g, int m, int n, f32x4 v0, f32x4 v1,
-                                                const float* bn, f32x4 c0, f32x4 c1, float lmu, float lrs,
-                                                const float* lg, const float* lb, bool first, float& s1,
-                                                float& s2) {
-#pragma clang fp contract(off)
+                                                const float* bn, f32x4 c0, f32x4 c1) {
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     v0[r] += bn[r];
     v1[r] += bn[4 + r];
-    if constexpr ((EPI & EPI_RESLN) != 0) {
-      c0[r] = __builtin_fmaf((c0[r] - lmu) * lrs, lg[r], lb[r]);
-      c1[r] = __builtin_fmaf((c1[r] - lmu) * lrs, lg[4 + r], lb[4 + r]);
-    }
     c0[r] += v0[r];
     c1[r] += v1[r];
   }
-  const size_t o = (size_t)m * g.ldc + n;
-  f32x4* p = (f32x4*)((float*)g.C + o);
+  f32x4* p = (f32x4*)((float*)g.C + (size_t)m * g.ldc + n);
   p[0] = c0;
   p[1] = c1;
-  if constexpr ((EPI & EPI_STATS) != 0) {
-    half8 h;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      h[r] = (_Float16)c0[r];
-      h[4 + r] = (_Float16)c1[r];
-    }
-    *(half8*)(g.c16 + o) = h;
-    float S = 0.f, Q = 0.f;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) S += c0[r];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) S += c1[r];
-    const float m8 = S * 0.125f;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float d = c0[r] - m8;
-      Q = __builtin_fmaf(d, d, Q);
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float d = c1[r] - m8;
-      Q = __builtin_fmaf(d, d, Q);
-    }
-    if (first) {
-      s1 = S;
-      s2 = Q;
-    } else {  // 8 + 8 values: M2 = M2a + M2b + (Sa - Sb)^2 / 16
-      const float d = s1 - S;
-      s2 = (s2 + Q) + d * d * 0.0625f;
-      s1 = s1 + S;
-    }
-  }
-}
-
-// LayerNorm statistics of row m from its P partials (sum S_p, M2_p over n = D / P values each;
-// EPI_FOLD / EPI_RESLN): mu = sum S_p / D, var = sum_p (M2_p + (S_p - n mu)^2 / n) / D (Chan's
-// merge: no E[x^2] - mu^2 cancellation). The four lanes that hold row m (lane groups fq = 0..3,
-// same fr) take partials fq, fq + 4, fq + 8, fq + 12 (P <= 16, D <= 1024) and combine with two
-// butterflies: every lane of the row gets the same (mu, r), and the order depends only on P —
-// not on the kernel or the batch size.
-__device__ __forceinline__ void ln_row_stats(const GemmArgs& g, int m, int fq, float& mu, float& rs) {
-#pragma clang fp contract(off)
-  const float2* st = g.st_in + (size_t)m * g.st_in_p;
-  float2 t[4];
-  float a = 0.f;
-#pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const int p = fq + 4 * u;
-    t[u] = p < g.st_in_p ? st[p] : make_float2(0.f, 0.f);
-    a += t[u].x;
-  }
-  a += __shfl_xor(a, 16);
-  a += __shfl_xor(a, 32);
-  const float inv = 1.0f / (float)g.ln_d;
-  mu = a * inv;
-  const float np = (float)(g.ln_d / g.st_in_p), inv_np = 1.0f / np;
-  float b = 0.f;
-#pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    if (fq + 4 * u < g.st_in_p) {
-      const float d = t[u].x - np * mu;
-      b += t[u].y + d * d * inv_np;
-    }
-  }
-  b += __shfl_xor(b, 16);
-  b += __shfl_xor(b, 32);
-  rs = rsqrtf(b * inv + g.ln_eps);
-}
-
-// EPI_FOLD: acc' = r (acc - mu colsum[n]) for eight columns (before bias and activation)
-__device__ __forceinline__ void ln_fold8(f32x4& v0, f32x4& v1, float mu, float rs, const float* cs) {
-#pragma clang fp contract(off)
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    v0[r] = __builtin_fmaf(-mu, cs[r], v0[r]) * rs;
-    v1[r] = __builtin_fmaf(-mu, cs[4 + r], v1[r]) * rs;
-  }
-}
-
-// EPI_STATS: this wave's 64-column slab partial (sum, M2) of row m from the lanes' (s1, s2) over
-// 16 values each (lane groups fq = 0..3 hold columns 8 fq .. 8 fq + 7 and 32 + 8 fq .. + 7),
-// merged by Chan's formula over the xor-16 then xor-32 partner (equal counts 16, 32: M2 = M2a +
-// M2b + (Sa - Sb)^2 / 2n, the same value on both partners); written by fq == 0. All 64 lanes must
-// execute it (shuffles).
-__device__ __forceinline__ void ln_slab_stats(const GemmArgs& g, int m, int slab, int fq, float s1, float s2) {
-#pragma clang fp contract(off)
-  float o1 = __shfl_xor(s1, 16), o2 = __shfl_xor(s2, 16);
-  float d = s1 - o1;
-  s2 = (s2 + o2) + d * d * (1.0f / 32.0f);
-  s1 = s1 + o1;
-  o1 = __shfl_xor(s1, 32);
-  o2 = __shfl_xor(s2, 32);
-  d = s1 - o1;
-  s2 = (s2 + o2) + d * d * (1.0f / 64.0f);
-  s1 = s1 + o1;
-  if (fq == 0 && m < g.M) g.st_out[(size_t)m * (g.N >> 6) + slab] = make_float2(s1, s2);
-}
-
-// eight consecutive floats (16-byte aligned)
-__device__ __forceinline__ void load8(const float* p, float (&v)[8]) {
-  const f32x4 a = ((const f32x4*)p)[0], b = ((const f32x4*)p)[1];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    v[r] = a[r];
-    v[4 + r] = b[r];
-  }
 }
 
 __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
@@ -241,14 +150,6 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 
 // fragment offset (bytes) of row j, 16-byte chunk c, in a swizzled 128-byte-row LDS image
 __device__ __forceinline__ int swz_off(int j, int c) { return j * 128 + ((c ^ ((j >> 1) & 7)) * 16); }
-
-// column (within a 32-column half of a wave's 64-column slab) of weight LDS row jj: lane group f
-// of the 16 x 16 MFMA block pair jb = 0, 1 owns 8 consecutive columns (one 16-byte f16 store),
-// in both GEMM kernels — so a row's EPI_STATS partials are summed in the same order by both
-__device__ __forceinline__ int g8_colperm(int jj) {
-  const int jb = jj >> 4, f = (jj >> 2) & 3, r = jj & 3;
-  return 8 * f + 4 * jb + r;
-}
 
 constexpr int GM = 128, GN = 128, GK = 64;
 constexpr int GTHREADS = 256;
@@ -285,9 +186,8 @@ __global__ __launch_bounds__(GTHREADS) void gemm_nt_kernel(GemmArgs g) {
       if (P < 16) {
         const int m = min(m0 + row, g.M - 1);
         src = g.A + (size_t)m * g.lda + k0 + c * 8;
-      } else {  // weight LDS row -> tile column: the block-pair permutation of K3d (g8_colperm)
-        const int col = (row & ~31) + g8_colperm(row & 31);
-        src = g.W + (size_t)(n0 + col) * g.ldw + k0 + c * 8;
+      } else {
+        src = g.W + (size_t)(n0 + row) * g.ldw + k0 + c * 8;
       }
       glds_x4(src, lds_base + buf * STAGE_BYTES + P * 1024);
     }
@@ -335,59 +235,44 @@ __global__ __launch_bounds__(GTHREADS) void gemm_nt_kernel(GemmArgs g) {
     __syncthreads();
   }
 
-  // epilogue over block pairs p (blocks 2p, 2p + 1: lane group fq owns columns 32 p + 8 fq + 0..7
-  // of the wave's slab); bias (and colsum / gamma / beta) as 16-byte loads; for the residual,
-  // every old C block of the wave in one batch of loads (rows clamped into the matrix) before
-  // the first store — loads issued between stores that may alias them cost one memory round
-  // trip per block
-  constexpr bool RES = epi_base(EPI) == EPI_F32_RESIDUAL;
-  const int nw0 = n0 + wc * 64 + 8 * fq;
-  float mu[4], rs[4];  // EPI_FOLD / EPI_RESLN: LayerNorm statistics of the lane's rows
-  if constexpr ((EPI & (EPI_FOLD | EPI_RESLN)) != 0) {
+  // epilogue: bias as one 16-byte load per column block; for the residual, every old C block of
+  // the wave in one batch of loads (rows clamped into the matrix) before the first store — loads
+  // issued between stores that may alias them cost one memory round trip per block
+  f32x4 bv[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) ln_row_stats(g, min(m0 + wr * 64 + 16 * i + fr, g.M - 1), fq, mu[i], rs[i]);
+  for (int j = 0; j < 4; ++j) bv[j] = f32x4{};
+  if (g.bias) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bv[j] = *(const f32x4*)(g.bias + n0 + wc * 64 + 16 * j + 4 * fq);
   }
-  float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+  f32x4 cv[4][4];
+  if constexpr (EPI == EPI_F32_RESIDUAL) {
 #pragma unroll
-  for (int p = 0; p < 2; ++p) {
-    const int n = nw0 + 32 * p;
-    float bn[8], cs[8], lg[8], lb[8];
-    if (g.bias)
-      load8(g.bias + n, bn);
-    else
-#pragma unroll
-      for (int r = 0; r < 8; ++r) bn[r] = 0.f;
-    if constexpr ((EPI & EPI_FOLD) != 0) load8(g.colsum + n, cs);
-    if constexpr ((EPI & EPI_RESLN) != 0) {
-      load8(g.ln_g + n, lg);
-      load8(g.ln_b + n, lb);
-    }
-    f32x4 cv[4][2];  // the pair's old C blocks, one batch of loads
-    if constexpr (RES) {
+    for (int j = 0; j < 4; ++j)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int mc = min(m0 + wr * 64 + 16 * i + fr, g.M - 1);
-        const f32x4* q = (const f32x4*)((const float*)g.C + (size_t)mc * g.ldc + n);
-        cv[i][0] = q[0];
-        cv[i][1] = q[1];
+        cv[i][j] = *(const f32x4*)((const float*)g.C + (size_t)mc * g.ldc + n0 + wc * 64 + 16 * j + 4 * fq);
       }
-    }
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int n = n0 + wc * 64 + 16 * j + 4 * fq;
+    const float bn[4] = {bv[j][0], bv[j][1], bv[j][2], bv[j][3]};
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int m = m0 + wr * 64 + 16 * i + fr;
-      f32x4 v0 = acc[i][2 * p], v1 = acc[i][2 * p + 1];
-      if constexpr ((EPI & EPI_FOLD) != 0) ln_fold8(v0, v1, mu[i], rs[i], cs);
-      if constexpr (RES) {
-        if (m < g.M)
-          gemm_store8_res<EPI>(g, m, n, v0, v1, bn, cv[i][0], cv[i][1], mu[i], rs[i], lg, lb, p == 0, s1[i], s2[i]);
-      } else if (m < g.M) {
-        gemm_store8<EPI>(g, m, n, v0, v1, bn);
+      if (m < g.M) {
+        if constexpr (EPI == EPI_F32_RESIDUAL) {
+          f32x4 c = cv[i][j], v = acc[i][j];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) c[r] += v[r] + bn[r];
+          *(f32x4*)((float*)g.C + (size_t)m * g.ldc + n) = c;
+        } else {
+          gemm_store4<EPI>(g, m, n, acc[i][j], bn);
+        }
       }
     }
-  }
-  if constexpr ((EPI & EPI_STATS) != 0) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) ln_slab_stats(g, m0 + wr * 64 + 16 * i + fr, (n0 >> 6) + wc, fq, s1[i], s2[i]);
   }
 }
 
@@ -438,12 +323,17 @@ struct G8Geom {
   static_assert(2 * SA + 2 * SB == G8_BUF, "a K-tile is 64 KiB");
   static_assert(NJ == 2, "column permutation below");
 };
+// tile column (within a wave-column half) of B LDS row jj: lane group f of the 16 x 16 MFMA
+// block pair jb = 0, 1 owns 8 consecutive columns (one 16-byte f16 store)
+__device__ __forceinline__ int g8_colperm(int jj) {
+  const int jb = jj >> 4, f = (jj >> 2) & 3, r = jj & 3;
+  return 8 * f + 4 * jb + r;
+}
+
 #define MRAG_VMCNT_CASE(n) \
   case n: asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory"); break;
-// n wave-uniform; a count above the 6-bit field waits for 63 (stricter: the wait is for "at
-// most n younger operations outstanding", so a smaller n only waits longer)
-__device__ __forceinline__ void vmcnt_wait(int n) {
-  switch (n > 63 ? 63 : n) {
+__device__ __forceinline__ void vmcnt_wait(int n) {  // n wave-uniform, 0..63
+  switch (n) {
     MRAG_VMCNT_CASE(1) MRAG_VMCNT_CASE(2) MRAG_VMCNT_CASE(3) MRAG_VMCNT_CASE(4) MRAG_VMCNT_CASE(5)
     MRAG_VMCNT_CASE(6) MRAG_VMCNT_CASE(7) MRAG_VMCNT_CASE(8) MRAG_VMCNT_CASE(9) MRAG_VMCNT_CASE(10)
     MRAG_VMCNT_CASE(11) MRAG_VMCNT_CASE(12) MRAG_VMCNT_CASE(13) MRAG_VMCNT_CASE(14) MRAG_VMCNT_CASE(15)
@@ -465,8 +355,8 @@ __device__ __forceinline__ void vmcnt_wait(int n) {
 // compiler lowers to a compare/branch tree of ~20 scalar instructions per call)
 template <int N>
 __device__ __forceinline__ void vmcnt_wait_c() {
-  static_assert(N >= 0, "vmcnt count");
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N > 63 ? 63 : N) : "memory");  // 6-bit field (see vmcnt_wait)
+  static_assert(N >= 0 && N < 64, "vmcnt field is 6 bits");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
 template <int EPI>
@@ -616,10 +506,7 @@ __global__ __launch_bounds__(G8_THREADS) void gemm_8p_kernel(GemmArgs g) {
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
   };
-  // vector stores per valid 8-column block (f16: one; f32: two; EPI_STATS: + the f16 copy) and
-  // per tile (EPI_STATS: + one partial per row block)
-  constexpr int SPB = (epi_base(EPI) >= EPI_F32_RESIDUAL ? 2 : 1) + ((EPI & EPI_STATS) ? 1 : 0);
-  constexpr int ST_FULL = SPB * 2 * 2 * NI + ((EPI & EPI_STATS) ? 2 * NI : 0);
+  constexpr int ST_FULL = ((EPI == EPI_F32_RESIDUAL || EPI == EPI_F32) ? 2 : 1) * 2 * 2 * NI;
   int st_phi = -100;  // last phase before the most recent epilogue
   int st_cnt = 0;     // vector stores that epilogue issued (wave-uniform)
   // end of a read segment: issue L[phi + 7] (slot SL), wait for L[phi + 2] (read by phase
@@ -702,79 +589,43 @@ __global__ __launch_bounds__(G8_THREADS) void gemm_8p_kernel(GemmArgs g) {
     // + (0..7) from the block pair jb = 0, 1 (one 16-byte f16 store, two for f32)
     const int tm = T / tiles_n;
     const int m0 = tm * BM, n0 = (T - tm * tiles_n) * BN;
-    float mu[2][NI], rs[2][NI];  // EPI_FOLD / EPI_RESLN: LayerNorm statistics of the lane's rows
-    if constexpr ((EPI & (EPI_FOLD | EPI_RESLN)) != 0) {
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int i = 0; i < NI; ++i)
-          ln_row_stats(g, min(m0 + WM * wr + HM * h + 16 * i + fr, g.M - 1), fq, mu[h][i], rs[h][i]);
-    }
-    float s1[2][NI], s2[2][NI];  // EPI_STATS: the lane's sums over its 16 columns of each row
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-      for (int i = 0; i < NI; ++i) s1[h][i] = s2[h][i] = 0.f;
+    constexpr int SPB = (EPI == EPI_F32_RESIDUAL || EPI == EPI_F32) ? 2 : 1;
 #pragma unroll
     for (int hh = 0; hh < 2; ++hh) {
       const int n = n0 + WN * wc + HN * hh + 8 * fq;
-      float bn[8], cs[8], lg[8], lb[8];
+      float bn[8];
 #pragma unroll
       for (int r = 0; r < 8; ++r) bn[r] = sbias[n + r];
-      if constexpr ((EPI & EPI_FOLD) != 0) load8(g.colsum + n, cs);
-      if constexpr ((EPI & EPI_RESLN) != 0) {
-        load8(g.ln_g + n, lg);
-        load8(g.ln_b + n, lb);
-      }
-      // residual: the old C values in one batch of loads per half (rows clamped into the matrix);
-      // with EPI_STATS one batch per (half, h), which keeps the epilogue within the registers
-      constexpr int CVB = (EPI & EPI_STATS) ? 1 : 2;  // h values per batch
+      // residual: the half's old C values in one batch of loads (rows clamped into the matrix)
       f32x4 cv[2][NI][2];
-      auto load_cv = [&](int h) {
+      if constexpr (EPI == EPI_F32_RESIDUAL) {
 #pragma unroll
-        for (int i = 0; i < NI; ++i) {
-          const int mc = min(m0 + WM * wr + HM * h + 16 * i + fr, g.M - 1);
-          const f32x4* p = (const f32x4*)((const float*)g.C + (size_t)mc * g.ldc + n);
-          cv[CVB == 1 ? 0 : h][i][0] = p[0];
-          cv[CVB == 1 ? 0 : h][i][1] = p[1];
-        }
-      };
-      if constexpr (epi_base(EPI) == EPI_F32_RESIDUAL && CVB == 2) {
-        load_cv(0);
-        load_cv(1);
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int i = 0; i < NI; ++i) {
+            const int mc = min(m0 + WM * wr + HM * h + 16 * i + fr, g.M - 1);
+            const f32x4* p = (const f32x4*)((const float*)g.C + (size_t)mc * g.ldc + n);
+            cv[h][i][0] = p[0];
+            cv[h][i][1] = p[1];
+          }
       }
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        if constexpr (epi_base(EPI) == EPI_F32_RESIDUAL && CVB == 1) load_cv(h);
-        const int hc = CVB == 1 ? 0 : h;
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
           const int mb = m0 + WM * wr + HM * h + 16 * i;  // wave-uniform block row
           const int m = mb + fr;
-          f32x4 v0 = acc[h][hh][i][0], v1 = acc[h][hh][i][1];
-          if constexpr ((EPI & EPI_FOLD) != 0) ln_fold8(v0, v1, mu[h][i], rs[h][i], cs);
           if (mb < g.M) {  // uniform branch: a block with a valid row issues exactly
             st_cnt += SPB;  // SPB vector stores (counted for the vmcnt bookkeeping)
             if (m < g.M) {
-              if constexpr (epi_base(EPI) == EPI_F32_RESIDUAL)
-                gemm_store8_res<EPI>(g, m, n, v0, v1, bn, cv[hc][i][0], cv[hc][i][1], mu[h][i], rs[h][i], lg, lb,
-                                     hh == 0, s1[h][i], s2[h][i]);
+              if constexpr (EPI == EPI_F32_RESIDUAL)
+                gemm_store8_res(g, m, n, acc[h][hh][i][0], acc[h][hh][i][1], bn, cv[h][i][0], cv[h][i][1]);
               else
-                gemm_store8<EPI>(g, m, n, v0, v1, bn);
+                gemm_store8<EPI>(g, m, n, acc[h][hh][i][0], acc[h][hh][i][1], bn);
             }
           }
         }
       }
-    }
-    if constexpr ((EPI & EPI_STATS) != 0) {
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int i = 0; i < NI; ++i) {
-          const int mb = m0 + WM * wr + HM * h + 16 * i;
-          ln_slab_stats(g, mb + fr, (n0 >> 6) + wc, fq, s1[h][i], s2[h][i]);
-          if (mb < g.M) st_cnt += 1;  // lane 0 (fq = 0, row mb) stores: one vector store
-        }
     }
   }
   if (wr == 0) bar();  // same barrier count for both groups
@@ -837,34 +688,8 @@ __device__ __forceinline__ void ln_params4(int lane, int D, const float* gamma, 
   }
 }
 
-// (sum, M2) of a wave's row of D values held as float4 chunks (zero past the row), two-pass from
-// registers, xor butterflies; lane 0 writes the row's single partial (st_in_p = 1 for the next
-// GEMM)
-__device__ __forceinline__ void row_stats_out(const f32x4 (&y)[4], int lane, int D, float2* st) {
-#pragma clang fp contract(off)
-  float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-#pragma unroll
-    for (int t = 0; t < 4; ++t) s1 += y[j][t];
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) s1 += __shfl_xor(s1, off);
-  const float mean = s1 / (float)D;
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-    if (lane + 64 * j < (D >> 2))
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const float d = y[j][t] - mean;
-        s2 = __builtin_fmaf(d, d, s2);
-      }
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) s2 += __shfl_xor(s2, off);
-  if (lane == 0) *st = make_float2(s1, s2);
-}
-
 __device__ __forceinline__ void ln_row4p(f32x4 (&v)[4], int lane, int D, float eps, const f32x4 (&g4)[4],
-                                         const f32x4 (&b4)[4], float* y32, _Float16* y16, float2* st = nullptr) {
+                                         const f32x4 (&b4)[4], float* y32, _Float16* y16) {
   typedef _Float16 half4 __attribute__((ext_vector_type(4)));
   const int nc = D >> 2;
   float s = 0.f;
@@ -887,16 +712,13 @@ __device__ __forceinline__ void ln_row4p(f32x4 (&v)[4], int lane, int D, float e
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) q += __shfl_xor(q, off);
   const float rstd = rsqrtf(q / (float)D + eps);
-  f32x4 ys[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int c = lane + 64 * j;
-    ys[j] = f32x4{};
     if (c < nc) {
       f32x4 y;
 #pragma unroll
       for (int t = 0; t < 4; ++t) y[t] = (v[j][t] - mean) * rstd * g4[j][t] + b4[j][t];
-      ys[j] = y;
       if (y32) ((f32x4*)y32)[c] = y;
       if (y16) {
         half4 h;
@@ -906,14 +728,13 @@ __device__ __forceinline__ void ln_row4p(f32x4 (&v)[4], int lane, int D, float e
       }
     }
   }
-  if (st) row_stats_out(ys, lane, D, st);
 }
 
 __device__ __forceinline__ void ln_row4(f32x4 (&v)[4], int lane, int D, float eps, const float* gamma,
-                                        const float* beta, float* y32, _Float16* y16, float2* st = nullptr) {
+                                        const float* beta, float* y32, _Float16* y16) {
   f32x4 g4[4], b4[4];
   ln_params4(lane, D, gamma, beta, g4, b4);
-  ln_row4p(v, lane, D, eps, g4, b4, y32, y16, st);
+  ln_row4p(v, lane, D, eps, g4, b4, y32, y16);
 }
 
 // One wave per row: the row's loads and the gamma / beta chunks are issued before the first
@@ -974,14 +795,12 @@ __global__ __launch_bounds__(256) void layernorm_stream_kernel(LayerNormArgs a) 
 }
 
 // ViT token assembly + pre_layrnorm in one pass (modeling_clip.py:212-217, :642):
-// X[b*T + t] = LN((t == 0 ? cls : patch[b*(T-1) + t-1]) + pos[t])   (f32), with its f16 copy X16
-// and row statistics st (one partial per row) for the first layer's folded LayerNorm
+// X[b*T + t] = LN((t == 0 ? cls : patch[b*(T-1) + t-1]) + pos[t])   (f32)
 __global__ __launch_bounds__(256) void vit_embed_ln_kernel(const float* __restrict__ patch,
                                                            const float* __restrict__ cls,
                                                            const float* __restrict__ pos, const float* gamma,
-                                                           const float* beta, float* __restrict__ X,
-                                                           _Float16* __restrict__ X16, float2* __restrict__ st, int B,
-                                                           int T, int D, float eps) {
+                                                           const float* beta, float* __restrict__ X, int B, int T,
+                                                           int D, float eps) {
   const int lane = threadIdx.x & 63;
   const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (r >= B * T) return;
@@ -999,7 +818,7 @@ __global__ __launch_bounds__(256) void vit_embed_ln_kernel(const float* __restri
       for (int u = 0; u < 4; ++u) v[j][u] = a[u] + q[u];
     }
   }
-  ln_row4(v, lane, D, eps, gamma, beta, X + (size_t)r * D, X16 ? X16 + (size_t)r * D : nullptr, st ? st + r : nullptr);
+  ln_row4(v, lane, D, eps, gamma, beta, X + (size_t)r * D, nullptr);
 }
 
 // ---------------------------------------------------------------------------
@@ -1330,18 +1149,12 @@ __global__ __launch_bounds__(256) void vit_im2col32_kernel(const uint8_t* __rest
 }
 
 // Token embeddings: X[b*T+t] = tok[ids] + pos[t] (+ type0 for BERT)   (f32)
-// one wave per token row (float4 over D <= 1024): X[bt] = tok[id] + pos[t] (+ type row); with
-// X16 / st (CLIP text: the first layer's LayerNorm is folded into its q|k|v GEMM) also the f16
-// copy and the row's statistics (one partial)
-__global__ __launch_bounds__(256) void token_embed_kernel(const int32_t* __restrict__ ids, const float* __restrict__ tok,
+// one workgroup per token row (float4 over D): X[bt] = tok[id] + pos[t] (+ type row)
+__global__ __launch_bounds__(128) void token_embed_kernel(const int32_t* __restrict__ ids, const float* __restrict__ tok,
                                                           const float* __restrict__ pos, const float* __restrict__ type_tab,
-                                                          const int32_t* __restrict__ types, float* __restrict__ X,
-                                                          _Float16* __restrict__ X16, float2* __restrict__ st, int B,
+                                                          const int32_t* __restrict__ types, float* __restrict__ X, int B,
                                                           int T, int D, int vocab) {
-  typedef _Float16 half4 __attribute__((ext_vector_type(4)));
-  const int lane = threadIdx.x & 63;
-  const int bt = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (bt >= B * T) return;
+  const int bt = blockIdx.x;
   const int t = bt % T;
   int id = ids[bt];
   id = id < 0 ? 0 : (id >= vocab ? vocab - 1 : id);
@@ -1349,60 +1162,16 @@ __global__ __launch_bounds__(256) void token_embed_kernel(const int32_t* __restr
   const f32x4* p = (const f32x4*)(pos + (size_t)t * D);
   const f32x4* ty = type_tab ? (const f32x4*)(type_tab + (size_t)(types ? (types[bt] != 0) : 0) * D) : nullptr;
   f32x4* o = (f32x4*)(X + (size_t)bt * D);
-  f32x4 ys[4];
+  for (int c = threadIdx.x; c < (D >> 2); c += blockDim.x) {
+    f32x4 v = e[c], q = p[c];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int c = lane + 64 * j;
-    ys[j] = f32x4{};
-    if (c < (D >> 2)) {
-      f32x4 v = e[c], q = p[c];
+    for (int u = 0; u < 4; ++u) v[u] += q[u];
+    if (ty) {  // BERT type_vocab_size 2
+      const f32x4 w = ty[c];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) v[u] += q[u];
-      if (ty) {  // BERT type_vocab_size 2
-        const f32x4 w = ty[c];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) v[u] += w[u];
-      }
-      o[c] = v;
-      ys[j] = v;
-      if (X16) {
-        half4 h;
-#pragma unroll
-        for (int u = 0; u < 4; ++u) h[u] = (_Float16)v[u];
-        ((half4*)(X16 + (size_t)bt * D))[c] = h;
-      }
+      for (int u = 0; u < 4; ++u) v[u] += w[u];
     }
-  }
-  if (st) row_stats_out(ys, lane, D, st + bt);
-}
-
-// Fold a LayerNorm (gamma, beta over K) into the GEMM that consumes it (see EPI_FOLD):
-// Wf[n][k] = f16(W[n][k] gamma[k]), bf[n] = bias[n] + sum_k W[n][k] beta[k], cs[n] = sum_k Wf[n][k]
-// (the folded f16 values, so acc - mu cs subtracts mu times exactly the weights the MFMA used).
-// One wave per output row, run once per weight upload.
-__global__ __launch_bounds__(256) void ln_fold_weight_kernel(const _Float16* __restrict__ W, const float* __restrict__ gamma,
-                                                             const float* __restrict__ beta, const float* __restrict__ bias,
-                                                             int N, int K, _Float16* __restrict__ Wf,
-                                                             float* __restrict__ bf, float* __restrict__ cs) {
-  const int lane = threadIdx.x & 63;
-  const int n = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (n >= N) return;
-  double sb = 0.0, sc = 0.0;
-  for (int k = lane; k < K; k += 64) {
-    const float w = (float)W[(size_t)n * K + k];
-    const _Float16 wf = (_Float16)(w * gamma[k]);
-    Wf[(size_t)n * K + k] = wf;
-    sc += (double)(float)wf;
-    sb += (double)w * (double)beta[k];
-  }
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    sc += __shfl_xor(sc, off);
-    sb += __shfl_xor(sb, off);
-  }
-  if (lane == 0) {
-    cs[n] = (float)sc;
-    bf[n] = (float)((bias ? (double)bias[n] : 0.0) + sb);
+    o[c] = v;
   }
 }
 
@@ -1477,7 +1246,7 @@ bool k3_beats_k3d(const GemmArgs& g) {
   return 2 * r_3 < 3 * r_d;  // K3 time ~ (2/3) r_3 < r_d
 }
 
-template <template <int> class KERN, bool RESLN_OK = true>
+template <template <int> class KERN>
 int launch_epi(int epi, dim3 grid, dim3 block, hipStream_t s, const GemmArgs& g) {
   switch (epi) {
     case EPI_F16: hipLaunchKernelGGL(KERN<EPI_F16>::fn, grid, block, 0, s, g); break;
@@ -1485,23 +1254,6 @@ int launch_epi(int epi, dim3 grid, dim3 block, hipStream_t s, const GemmArgs& g)
     case EPI_F16_GELU_ERF: hipLaunchKernelGGL(KERN<EPI_F16_GELU_ERF>::fn, grid, block, 0, s, g); break;
     case EPI_F32_RESIDUAL: hipLaunchKernelGGL(KERN<EPI_F32_RESIDUAL>::fn, grid, block, 0, s, g); break;
     case EPI_F32: hipLaunchKernelGGL(KERN<EPI_F32>::fn, grid, block, 0, s, g); break;
-    case EPI_F16 | EPI_FOLD: hipLaunchKernelGGL(KERN<EPI_F16 | EPI_FOLD>::fn, grid, block, 0, s, g); break;
-    case EPI_F16_QUICK_GELU | EPI_FOLD:
-      hipLaunchKernelGGL(KERN<EPI_F16_QUICK_GELU | EPI_FOLD>::fn, grid, block, 0, s, g);
-      break;
-    case EPI_F16_GELU_ERF | EPI_FOLD:
-      hipLaunchKernelGGL(KERN<EPI_F16_GELU_ERF | EPI_FOLD>::fn, grid, block, 0, s, g);
-      break;
-    case EPI_F32_RESIDUAL | EPI_STATS:
-      hipLaunchKernelGGL(KERN<EPI_F32_RESIDUAL | EPI_STATS>::fn, grid, block, 0, s, g);
-      break;
-    case EPI_F32_RESIDUAL | EPI_STATS | EPI_RESLN:
-      if constexpr (RESLN_OK) {
-        hipLaunchKernelGGL(KERN<EPI_F32_RESIDUAL | EPI_STATS | EPI_RESLN>::fn, grid, block, 0, s, g);
-        break;
-      } else {
-        return mrag::fail(MRAG_ERR_ARG, "gemm: epilogue %d has no K3d instance", epi);
-      }
     default: return mrag::fail(MRAG_ERR_ARG, "gemm: bad epilogue %d", epi);
   }
   MRAG_CHECK_LAUNCH();
@@ -1522,18 +1274,10 @@ int launch_gemm(const GemmArgs& g, int epi, hipStream_t s) {
                GK);
   MRAG_REQUIRE(g.lda % 8 == 0 && g.ldw % 8 == 0 && g.ldc % 4 == 0, "gemm: lda/ldw must be multiples of 8, ldc of 4");
   MRAG_REQUIRE(((uintptr_t)g.bias & 15) == 0 && ((uintptr_t)g.C & 15) == 0, "gemm: bias and C must be 16-byte aligned");
-  if (epi & (EPI_FOLD | EPI_RESLN))
-    MRAG_REQUIRE(g.st_in && g.st_in_p > 0 && g.ln_d > 0 && ((epi & EPI_FOLD) == 0 || g.colsum) &&
-                     ((epi & EPI_RESLN) == 0 || (g.ln_g && g.ln_b)),
-                 "gemm: LayerNorm fold arguments missing");
-  if (epi & EPI_STATS)
-    MRAG_REQUIRE(g.c16 && g.st_out && g.N % 64 == 0 && ((uintptr_t)g.c16 & 15) == 0, "gemm: statistics outputs missing");
-  // EPI_RESLN (post-LN BERT residuals, N = 384 for MiniLM) has no K3d instance (its extra
-  // epilogue registers spill there)
-  if ((epi & EPI_RESLN) == 0 && g.M >= 1024 && g.N <= G8_BIAS_MAX && g.N % 256 == 0 && !k3_beats_k3d(g)) {
+  if (g.M >= 1024 && g.N <= G8_BIAS_MAX && g.N % 256 == 0 && !k3_beats_k3d(g)) {
     const int ntiles = ((g.M + G8Geom::BM - 1) / G8Geom::BM) * (g.N / G8Geom::BN);
     const int nb = std::min((ntiles + 7) / 8 * 8, std::max(8, num_cus() / 8 * 8));
-    return launch_epi<K3dKern, false>(epi, dim3((unsigned)nb), dim3(G8_THREADS), s, g);
+    return launch_epi<K3dKern>(epi, dim3((unsigned)nb), dim3(G8_THREADS), s, g);
   }
   const dim3 grid((unsigned)(((g.M + GM - 1) / GM) * (g.N / GN)));
   return launch_epi<K3Kern>(epi, grid, dim3(GTHREADS), s, g);
@@ -1561,11 +1305,11 @@ int launch_layernorm(const LayerNormArgs& a, hipStream_t s) {
 }
 
 int launch_vit_embed_ln(const float* patch, const float* cls, const float* pos, const float* gamma, const float* beta,
-                        float* X, _Float16* X16, float2* st, int B, int T, int D, float eps, hipStream_t s) {
+                        float* X, int B, int T, int D, float eps, hipStream_t s) {
   if (B * T == 0) return MRAG_OK;
   MRAG_REQUIRE(D % 4 == 0 && D <= 1024, "vit_embed_ln: D=%d unsupported", D);
   hipLaunchKernelGGL(vit_embed_ln_kernel, dim3((unsigned)((B * T + 3) / 4)), dim3(256), 0, s, patch, cls, pos, gamma,
-                     beta, X, X16, st, B, T, D, eps);
+                     beta, X, B, T, D, eps);
   MRAG_CHECK_LAUNCH();
   return MRAG_OK;
 }
@@ -1602,22 +1346,12 @@ int launch_vit_im2col(const uint8_t* img, _Float16* out, int B, int S, int P, hi
 }
 
 int launch_token_embed(const int32_t* ids, const float* tok, const float* pos, const float* type_tab,
-                       const int32_t* types, float* X, _Float16* X16, float2* st, int B, int T, int D, int vocab,
-                       hipStream_t s) {
+                       const int32_t* types, float* X, int B, int T, int D, int vocab, hipStream_t s) {
   const int64_t n = (int64_t)B * T;
   if (n == 0 || D == 0) return MRAG_OK;
-  MRAG_REQUIRE(D % 4 == 0 && D <= 1024 && n < (1ll << 31), "token_embed: D=%d must be a multiple of 4, <= 1024", D);
-  hipLaunchKernelGGL(token_embed_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, ids, tok, pos, type_tab, types,
-                     X, X16, st, B, T, D, vocab);
-  MRAG_CHECK_LAUNCH();
-  return MRAG_OK;
-}
-
-int launch_ln_fold_weight(const _Float16* W, const float* gamma, const float* beta, const float* bias, int N, int K,
-                          _Float16* Wf, float* bf, float* cs, hipStream_t s) {
-  if (N <= 0) return MRAG_OK;
-  hipLaunchKernelGGL(ln_fold_weight_kernel, dim3((unsigned)((N + 3) / 4)), dim3(256), 0, s, W, gamma, beta, bias, N, K,
-                     Wf, bf, cs);
+  MRAG_REQUIRE(D % 4 == 0 && n < (1ll << 31), "token_embed: D=%d must be a multiple of 4", D);
+  hipLaunchKernelGGL(token_embed_kernel, dim3((unsigned)n), dim3(128), 0, s, ids, tok, pos, type_tab, types, X, B, T,
+                     D, vocab);
   MRAG_CHECK_LAUNCH();
   return MRAG_OK;
 }

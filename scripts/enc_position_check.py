@@ -1,6 +1,7 @@
-"""Position / batch independence of the folded-LayerNorm encoders at reduced depth: a sequence
-alone vs inside a padded batch, per number of layers (which layer first breaks it), and the same
-batch twice (determinism)."""
+"""Position / batch independence of the encoders at reduced depth: a sequence alone vs inside a
+padded batch and two copies of one sequence at different row offsets, per number of layers
+(which layer first breaks it), and the same batch twice (determinism). Written to localise the
+round-4 LayerNorm-fold experiment's ulp-level position dependence (notes/gemm_experiments.md)."""
 import dataclasses
 import json
 import os
