@@ -1,0 +1,107 @@
+// Per-CU L2 -> LDS fill rate on gfx950: one workgroup per CU streams a per-XCD-shared,
+// L2-resident source region into a 64 KiB LDS ring, by (0) LDS-DMA global_load_lds_dwordx4,
+// (1) global_load_dwordx4 + ds_write_b128 (register staged), (2) global_load_dwordx4 only.
+// Waves 4 or 8, each keeping `depth` 1 KiB pieces in flight. Prints GB/s per CU.
+// Build: hipcc --offload-arch=gfx950 -O3 -o fill_rate fill_rate.hip
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+#define AS3 __attribute__((address_space(3)))
+
+__device__ __forceinline__ void glds_x4(const void* gsrc, uint32_t lds_addr) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(lds_addr)
+               : "memory");
+}
+
+template <int MODE, int DEPTH>
+__global__ __launch_bounds__(512) void fill_kernel(const char* __restrict__ src, size_t region, int iters,
+                                                   float* __restrict__ sink) {
+  __shared__ __attribute__((aligned(16))) char ring[65536];
+  const int lane = threadIdx.x & 63, nw = blockDim.x >> 6;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t base = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)((AS3 char*)ring));
+  // workgroups of one XCD (b mod 8) share one region (L2-resident after the first pass)
+  const char* r = src + (size_t)(blockIdx.x & 7) * region;
+  const int pieces = (int)(region / 1024);
+  f32x4 acc = {0, 0, 0, 0};
+  int p = w;
+  for (int it = 0; it < iters; ++it) {
+#pragma unroll
+    for (int d = 0; d < DEPTH; ++d) {
+      const int pc = (p + d * nw) % pieces;
+      const char* g = r + (size_t)pc * 1024 + lane * 16;
+      const uint32_t slot = (uint32_t)(((w * DEPTH + d) & 63) * 1024);
+      if constexpr (MODE == 0) {
+        glds_x4(g, __builtin_amdgcn_readfirstlane(base + slot));
+      } else {
+        const f32x4 v = *(const f32x4*)g;
+        if constexpr (MODE == 1) {
+          *(f32x4*)(ring + slot + lane * 16) = v;
+        } else {
+          acc += v;
+        }
+      }
+    }
+    p = (p + DEPTH * nw) % pieces;
+    if constexpr (MODE == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  if (MODE == 1) __syncthreads();
+  if (MODE != 0 || true) {
+    const float x = acc[0] + acc[1] + acc[2] + acc[3] + (float)((const float*)ring)[threadIdx.x];
+    if (x == 12345.678f) sink[blockIdx.x] = x;
+  }
+}
+
+template <int MODE, int DEPTH>
+float run(const char* src, size_t region, int nwg, int threads, int iters, float* sink) {
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0);
+  hipEventCreate(&e1);
+  hipLaunchKernelGGL((fill_kernel<MODE, DEPTH>), dim3(nwg), dim3(threads), 0, 0, src, region, 4, sink);
+  hipEventRecord(e0);
+  hipLaunchKernelGGL((fill_kernel<MODE, DEPTH>), dim3(nwg), dim3(threads), 0, 0, src, region, iters, sink);
+  hipEventRecord(e1);
+  hipEventSynchronize(e1);
+  float ms = 0;
+  hipEventElapsedTime(&ms, e0, e1);
+  const double bytes_per_wg = (double)iters * DEPTH * (threads / 64) * 1024.0;
+  return (float)(bytes_per_wg / (ms * 1e-3) / 1e9);
+}
+
+int main() {
+  int cus = 0;
+  hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
+  const int nwg = cus;  // one workgroup per CU (64 KiB LDS each + the ring -> 1 per CU)
+  const size_t region = 1 << 20;  // 1 MiB per XCD: L2-resident
+  char* src = nullptr;
+  float* sink = nullptr;
+  hipMalloc(&src, region * 8);
+  hipMemset(src, 1, region * 8);
+  hipMalloc(&sink, nwg * 4);
+  const int iters = 2000;
+  const char* names[3] = {"lds_dma", "reg_staged_ds_write", "reg_only"};
+  for (int threads : {256, 512}) {
+    float r[3][3];
+    r[0][0] = run<0, 2>(src, region, nwg, threads, iters, sink);
+    r[0][1] = run<0, 4>(src, region, nwg, threads, iters, sink);
+    r[0][2] = run<0, 8>(src, region, nwg, threads, iters, sink);
+    r[1][0] = run<1, 2>(src, region, nwg, threads, iters, sink);
+    r[1][1] = run<1, 4>(src, region, nwg, threads, iters, sink);
+    r[1][2] = run<1, 8>(src, region, nwg, threads, iters, sink);
+    r[2][0] = run<2, 2>(src, region, nwg, threads, iters, sink);
+    r[2][1] = run<2, 4>(src, region, nwg, threads, iters, sink);
+    r[2][2] = run<2, 8>(src, region, nwg, threads, iters, sink);
+    for (int m = 0; m < 3; ++m)
+      printf("{\"mode\": \"%s\", \"waves\": %d, \"gbs_per_cu_depth2\": %.1f, \"depth4\": %.1f, \"depth8\": %.1f}\n",
+             names[m], threads / 64, r[m][0], r[m][1], r[m][2]);
+  }
+  hipError_t e = hipDeviceSynchronize();
+  printf("{\"cus\": %d, \"status\": \"%s\"}\n", cus, hipGetErrorString(e));
+  return 0;
+}
