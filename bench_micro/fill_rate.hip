@@ -74,11 +74,11 @@ float run(const char* src, size_t region, int nwg, int threads, int iters, float
   return (float)(bytes_per_wg / (ms * 1e-3) / 1e9);
 }
 
-int main() {
+int main(int argc, char** argv) {
   int cus = 0;
   hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
   const int nwg = cus;  // one workgroup per CU (64 KiB LDS each + the ring -> 1 per CU)
-  const size_t region = 1 << 20;  // 1 MiB per XCD: L2-resident
+  const size_t region = (size_t)(argc > 1 ? atof(argv[1]) : 1.0) * (1 << 20);  // MiB per XCD (1: L2-resident)
   char* src = nullptr;
   float* sink = nullptr;
   hipMalloc(&src, region * 8);
@@ -98,8 +98,8 @@ int main() {
     r[2][1] = run<2, 4>(src, region, nwg, threads, iters, sink);
     r[2][2] = run<2, 8>(src, region, nwg, threads, iters, sink);
     for (int m = 0; m < 3; ++m)
-      printf("{\"mode\": \"%s\", \"waves\": %d, \"gbs_per_cu_depth2\": %.1f, \"depth4\": %.1f, \"depth8\": %.1f}\n",
-             names[m], threads / 64, r[m][0], r[m][1], r[m][2]);
+      printf("{\"region_mib_per_xcd\": %.1f, \"mode\": \"%s\", \"waves\": %d, \"gbs_per_cu_depth2\": %.1f, \"depth4\": %.1f, \"depth8\": %.1f}\n",
+             region / 1048576.0, names[m], threads / 64, r[m][0], r[m][1], r[m][2]);
   }
   hipError_t e = hipDeviceSynchronize();
   printf("{\"cus\": %d, \"status\": \"%s\"}\n", cus, hipGetErrorString(e));
