@@ -58,6 +58,32 @@ __global__ __launch_bounds__(512) void fill_kernel(const char* __restrict__ src,
   }
 }
 
+// GEMM-shaped fill (no compute): workgroup b streams the K-tiles of tile (tm, tn) of an
+// M x K activation / N x K weight pair like K3d: per 64-deep K-tile 32 A pieces (8 rows x 128 B of
+// its A panel, rows K * 2 bytes apart) and 32 W pieces, 8 per wave, then vmcnt(0)
+__global__ __launch_bounds__(512) void gemm_fill_kernel(const char* __restrict__ A, const char* __restrict__ W, int K,
+                                                        int tiles_m, int tiles_n, int passes, float* __restrict__ sink) {
+  __shared__ __attribute__((aligned(16))) char ring[65536];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t base = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)((AS3 char*)ring));
+  const int T = blockIdx.x % (tiles_m * tiles_n);
+  const int tm = T / tiles_n, tn = T % tiles_n;
+  const int rr = lane >> 3, pos = lane & 7;
+  const size_t ld = (size_t)K * 2;
+  for (int it = 0; it < passes; ++it)
+    for (int kt = 0; kt < K / 64; ++kt) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int P = 8 * w + i;
+        const char* g = P < 32 ? A + (size_t)(256 * tm + 8 * P + rr) * ld : W + (size_t)(256 * tn + 8 * (P - 32) + rr) * ld;
+        glds_x4(g + kt * 128 + pos * 16, __builtin_amdgcn_readfirstlane(base + (uint32_t)(P * 1024)));
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  if (((const float*)ring)[threadIdx.x] == 12345.678f) sink[blockIdx.x] = 1.f;
+}
+
 template <int MODE, int DEPTH>
 float run(const char* src, size_t region, int nwg, int threads, int iters, float* sink) {
   hipEvent_t e0, e1;
@@ -100,6 +126,27 @@ int main(int argc, char** argv) {
     for (int m = 0; m < 3; ++m)
       printf("{\"region_mib_per_xcd\": %.1f, \"mode\": \"%s\", \"waves\": %d, \"gbs_per_cu_depth2\": %.1f, \"depth4\": %.1f, \"depth8\": %.1f}\n",
              region / 1048576.0, names[m], threads / 64, r[m][0], r[m][1], r[m][2]);
+  }
+  {  // GEMM-shaped fills: qkv (12800 x 768 activations, 2304 x 768 weights), one tile per CU
+    const int K = 768, tm = 50, tn = 9, passes = 20;
+    char *Ab = nullptr, *Wb = nullptr;
+    hipMalloc(&Ab, (size_t)256 * tm * K * 2);
+    hipMalloc(&Wb, (size_t)256 * tn * K * 2);
+    hipMemset(Ab, 1, (size_t)256 * tm * K * 2);
+    hipMemset(Wb, 1, (size_t)256 * tn * K * 2);
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    hipLaunchKernelGGL(gemm_fill_kernel, dim3(nwg), dim3(512), 0, 0, Ab, Wb, K, tm, tn, 2, sink);
+    hipEventRecord(e0);
+    hipLaunchKernelGGL(gemm_fill_kernel, dim3(nwg), dim3(512), 0, 0, Ab, Wb, K, tm, tn, passes, sink);
+    hipEventRecord(e1);
+    hipEventSynchronize(e1);
+    float ms = 0;
+    hipEventElapsedTime(&ms, e0, e1);
+    const double bytes = (double)passes * (K / 64) * 64 * 1024.0;
+    printf("{\"mode\": \"gemm_shaped_lds_dma\", \"waves\": 8, \"depth\": 8, \"gbs_per_cu\": %.1f}\n",
+           bytes / (ms * 1e-3) / 1e9);
   }
   hipError_t e = hipDeviceSynchronize();
   printf("{\"cus\": %d, \"status\": \"%s\"}\n", cus, hipGetErrorString(e));
