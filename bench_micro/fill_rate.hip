@@ -62,12 +62,18 @@ __global__ __launch_bounds__(512) void fill_kernel(const char* __restrict__ src,
 // M x K activation / N x K weight pair like K3d: per 64-deep K-tile 32 A pieces (8 rows x 128 B of
 // its A panel, rows K * 2 bytes apart) and 32 W pieces, 8 per wave, then vmcnt(0)
 __global__ __launch_bounds__(512) void gemm_fill_kernel(const char* __restrict__ A, const char* __restrict__ W, int K,
-                                                        int tiles_m, int tiles_n, int passes, float* __restrict__ sink) {
+                                                        int tiles_m, int tiles_n, int passes, int xcd_group,
+                                                        float* __restrict__ sink) {
   __shared__ __attribute__((aligned(16))) char ring[65536];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t base = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)((AS3 char*)ring));
-  const int T = blockIdx.x % (tiles_m * tiles_n);
+  int T = blockIdx.x;
+  if (xcd_group) {  // blocks b, b + 8, ... (one XCD) take consecutive tile ids, as K3d does
+    const int nwg = gridDim.x, xcd = T & 7, q8 = nwg >> 3, r8 = nwg & 7;
+    T = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (T >> 3);
+  }
+  T %= tiles_m * tiles_n;
   const int tm = T / tiles_n, tn = T % tiles_n;
   const int rr = lane >> 3, pos = lane & 7;
   const size_t ld = (size_t)K * 2;
@@ -137,16 +143,18 @@ int main(int argc, char** argv) {
     hipEvent_t e0, e1;
     hipEventCreate(&e0);
     hipEventCreate(&e1);
-    hipLaunchKernelGGL(gemm_fill_kernel, dim3(nwg), dim3(512), 0, 0, Ab, Wb, K, tm, tn, 2, sink);
-    hipEventRecord(e0);
-    hipLaunchKernelGGL(gemm_fill_kernel, dim3(nwg), dim3(512), 0, 0, Ab, Wb, K, tm, tn, passes, sink);
-    hipEventRecord(e1);
-    hipEventSynchronize(e1);
-    float ms = 0;
-    hipEventElapsedTime(&ms, e0, e1);
-    const double bytes = (double)passes * (K / 64) * 64 * 1024.0;
-    printf("{\"mode\": \"gemm_shaped_lds_dma\", \"waves\": 8, \"depth\": 8, \"gbs_per_cu\": %.1f}\n",
-           bytes / (ms * 1e-3) / 1e9);
+    for (int xg = 0; xg < 2; ++xg) {
+      hipLaunchKernelGGL(gemm_fill_kernel, dim3(nwg), dim3(512), 0, 0, Ab, Wb, K, tm, tn, 2, xg, sink);
+      hipEventRecord(e0);
+      hipLaunchKernelGGL(gemm_fill_kernel, dim3(nwg), dim3(512), 0, 0, Ab, Wb, K, tm, tn, passes, xg, sink);
+      hipEventRecord(e1);
+      hipEventSynchronize(e1);
+      float ms = 0;
+      hipEventElapsedTime(&ms, e0, e1);
+      const double bytes = (double)passes * (K / 64) * 64 * 1024.0;
+      printf("{\"mode\": \"gemm_shaped_lds_dma\", \"xcd_grouped\": %d, \"waves\": 8, \"depth\": 8, "
+             "\"gbs_per_cu\": %.1f}\n", xg, bytes / (ms * 1e-3) / 1e9);
+    }
   }
   hipError_t e = hipDeviceSynchronize();
   printf("{\"cus\": %d, \"status\": \"%s\"}\n", cus, hipGetErrorString(e));

@@ -307,7 +307,8 @@ __global__ __launch_bounds__(GTHREADS) void gemm_nt_kernel(GemmArgs g) {
 // round-robin by its workgroups, so an A panel and the weight panels stay in that L2.
 // Timing-only ablation builds (results wrong; scripts/k3d_ablate.sh): bit 1 no LDS-DMA, 2 no
 // fragment reads, 4 no barrier after the MFMA segment, 8 no barrier after the read segment,
-// 16 no epilogue stores, 32 no MFMAs, 64 one reduced value per lane instead of the epilogue
+// 16 no epilogue stores, 32 no MFMAs, 64 one reduced value per lane instead of the epilogue,
+// 128 no s_setprio around the MFMA segments (timing and result-preserving A/B)
 #ifndef MRAG_K3D_ABL
 #define MRAG_K3D_ABL 0
 #endif
@@ -500,7 +501,7 @@ __global__ __launch_bounds__(G8_THREADS) void gemm_8p_kernel(GemmArgs g) {
   };
   auto mfma_q = [&](f32x4 (&a)[NI][NJ], const half8 (&fb)[NJ][2]) {
     if constexpr ((MRAG_K3D_ABL & 32) != 0) return;
-    __builtin_amdgcn_s_setprio(1);
+    if constexpr ((MRAG_K3D_ABL & 128) == 0) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll

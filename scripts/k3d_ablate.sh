@@ -6,7 +6,7 @@
 set -e
 R=$(cd "$(dirname "$0")/.." && pwd)
 P=$R/multimodal-rag-for-image-text-search_amd
-MASKS="${MASKS:-0 1 2 3 4 8 12 13 15 47 64 65 66 67 76}"
+MASKS="${MASKS:-0 1 2 3 4 8 12 13 15 47 64 65 66 67 76 128}"
 if [ "$1" = build ]; then
   make -C $P -j8 >/dev/null
   for m in $MASKS; do
