@@ -465,9 +465,10 @@ def fusion_leg(world: int, rank: int, local: int, steps: int, warmup: int):
     # overlap with other branches' and steps' work, as a serving process with concurrent query
     # batches runs them. At N > 1 everything stays in one thread: the collectives share one
     # communicator and must be issued in the same order on every rank. MRAG_FUSION_STREAMS=1
-    # serialises the branches, MRAG_FUSION_INFLIGHT sets the steps in flight (A/B timing).
+    # serialises the branches, MRAG_FUSION_INFLIGHT sets the steps in flight (A/B timing; four
+    # measured +2.8 % over two in five interleaved pairs, profiles/r4s24_fusion_inflight_ab.txt).
     two = world == 1 and os.environ.get("MRAG_FUSION_STREAMS", "2") != "1"
-    slots = max(1, int(os.environ.get("MRAG_FUSION_INFLIGHT", "2"))) if two else 1
+    slots = max(1, int(os.environ.get("MRAG_FUSION_INFLIGHT", "4"))) if two else 1
     from concurrent.futures import ThreadPoolExecutor
 
     class Slot:
