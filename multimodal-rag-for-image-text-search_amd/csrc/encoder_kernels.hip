@@ -305,13 +305,8 @@ __global__ __launch_bounds__(GTHREADS) void gemm_nt_kernel(GemmArgs g) {
 // which precedes every read of phase phi + 1 (RAW).
 // Tiles: XCD x (blocks b = x mod 8) owns a contiguous range of tile ids (tm-major), taken
 // round-robin by its workgroups, so an A panel and the weight panels stay in that L2.
-// Timing-only ablation builds (results wrong; scripts/k3d_ablate.sh): bit 1 no LDS-DMA, 2 no
-// fragment reads, 4 no barrier after the MFMA segment, 8 no barrier after the read segment,
-// 16 no epilogue stores, 32 no MFMAs, 64 one reduced value per lane instead of the epilogue,
-// 128 no s_setprio around the MFMA segments (timing and result-preserving A/B)
-#ifndef MRAG_K3D_ABL
-#define MRAG_K3D_ABL 0
-#endif
+// (The round-4 timing ablations of this kernel — profiles/r4_k3d_ablations.txt — were built
+// from commit 227f50e with scripts/k3d_ablate.sh; they are not part of the product source.)
 constexpr int G8_THREADS = 512;
 constexpr int G8_BUF = 65536;      // one K-tile: two A and two B half-tile slots
 constexpr int G8_BIAS_MAX = 4096;  // bias floats staged in LDS
@@ -455,7 +450,7 @@ __global__ __launch_bounds__(G8_THREADS) void gemm_8p_kernel(GemmArgs g) {
       else if constexpr (sl == 1) src = g.W + gB[0][q];
       else if constexpr (sl == 2) src = g.W + gB[1][q];
       else src = g.A + gA[1][q];
-      if constexpr ((MRAG_K3D_ABL & 1) == 0) glds_x4(src + k0, dst + q * 1024);
+      glds_x4(src + k0, dst + q * 1024);
     }
     if constexpr (sl == 3) {  // K-tile complete: advance the loader
       ld_par ^= 1;
@@ -482,7 +477,6 @@ __global__ __launch_bounds__(G8_THREADS) void gemm_8p_kernel(GemmArgs g) {
   f32x4 acc[2][2][NI][NJ];  // [h][hh][i][jb]
   half8 fa[NI][2], fb0[NJ][2], fb1[NJ][2];
   auto readA = [&](const char* slot) {
-    if constexpr ((MRAG_K3D_ABL & 2) != 0) return;
 #pragma unroll
     for (int i = 0; i < NI; ++i)
 #pragma unroll
@@ -491,7 +485,6 @@ __global__ __launch_bounds__(G8_THREADS) void gemm_8p_kernel(GemmArgs g) {
       }
   };
   auto readB = [&](const char* slot, half8 (&fb)[NJ][2]) {
-    if constexpr ((MRAG_K3D_ABL & 2) != 0) return;
 #pragma unroll
     for (int jb = 0; jb < NJ; ++jb)
 #pragma unroll
@@ -500,8 +493,7 @@ __global__ __launch_bounds__(G8_THREADS) void gemm_8p_kernel(GemmArgs g) {
       }
   };
   auto mfma_q = [&](f32x4 (&a)[NI][NJ], const half8 (&fb)[NJ][2]) {
-    if constexpr ((MRAG_K3D_ABL & 32) != 0) return;
-    if constexpr ((MRAG_K3D_ABL & 128) == 0) __builtin_amdgcn_s_setprio(1);
+    __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
@@ -544,7 +536,7 @@ __global__ __launch_bounds__(G8_THREADS) void gemm_8p_kernel(GemmArgs g) {
       vmcnt_wait(younger(phi + 2, total - 1) + (post ? st_cnt : 0));
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if constexpr ((MRAG_K3D_ABL & 8) == 0) bar();
+    bar();
   };
 
   {  // prologue: L[0..6], then L[0], L[1] landed
@@ -579,18 +571,18 @@ __global__ __launch_bounds__(G8_THREADS) void gemm_8p_kernel(GemmArgs g) {
       readB(buf + GG::slot_off(1), fb0);
       end_reads(phi, S3{});
       mfma_q(acc[0][0], fb0);
-      if constexpr ((MRAG_K3D_ABL & 4) == 0) bar();
+      bar();
       readB(buf + GG::slot_off(2), fb1);  // phase 1: (h0, hh1)
       end_reads(phi + 1, S0{});
       mfma_q(acc[0][1], fb1);
-      if constexpr ((MRAG_K3D_ABL & 4) == 0) bar();
+      bar();
       readA(buf + GG::slot_off(3));  // phase 2: (h1, hh1)
       end_reads(phi + 2, S1{});
       mfma_q(acc[1][1], fb1);
-      if constexpr ((MRAG_K3D_ABL & 4) == 0) bar();
+      bar();
       end_reads(phi + 3, S2{});  // phase 3: (h1, hh0) from registers
       mfma_q(acc[1][0], fb0);
-      if constexpr ((MRAG_K3D_ABL & 4) == 0) bar();
+      bar();
     }
     st_phi = phi - 1;
     st_cnt = 0;
@@ -599,19 +591,6 @@ __global__ __launch_bounds__(G8_THREADS) void gemm_8p_kernel(GemmArgs g) {
     // + (0..7) from the block pair jb = 0, 1 (one 16-byte f16 store, two for f32)
     const int tm = T / tiles_n;
     const int m0 = tm * BM, n0 = (T - tm * tiles_n) * BN;
-    if constexpr ((MRAG_K3D_ABL & 64) != 0) {  // ablation: one reduced value per lane, MFMAs kept live
-      float red = 0.f;
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int hh = 0; hh < 2; ++hh)
-#pragma unroll
-          for (int i = 0; i < NI; ++i)
-#pragma unroll
-            for (int jb = 0; jb < NJ; ++jb) red += acc[h][hh][i][jb][0] + acc[h][hh][i][jb][3];
-      if (red == 1234.5f) ((float*)g.C)[lane] = red;
-      continue;
-    }
     constexpr int SPB = (EPI == EPI_F32_RESIDUAL || EPI == EPI_F32) ? 2 : 1;
 #pragma unroll
     for (int hh = 0; hh < 2; ++hh) {
@@ -640,7 +619,7 @@ __global__ __launch_bounds__(G8_THREADS) void gemm_8p_kernel(GemmArgs g) {
           const int m = mb + fr;
           if (mb < g.M) {  // uniform branch: a block with a valid row issues exactly
             st_cnt += SPB;  // SPB vector stores (counted for the vmcnt bookkeeping)
-            if ((MRAG_K3D_ABL & 16) == 0 && m < g.M) {
+            if (m < g.M) {
               if constexpr (EPI == EPI_F32_RESIDUAL)
                 gemm_store8_res(g, m, n, acc[h][hh][i][0], acc[h][hh][i][1], bn, cv[h][i][0], cv[h][i][1]);
               else

@@ -49,7 +49,10 @@ constexpr int QPG = SCAN_WAVES * QPW;       // queries per workgroup
 constexpr int MAX_MERGE_ENTRIES = 4096;     // splits * KL cap (LDS sort in K8)
 constexpr int MAX_K = 256;
 constexpr int MERGE_THREADS = 256;
-constexpr int SAMPLE_STRIDE = 16;          // K7 sample pre-pass: every 16th tile of a split
+#ifndef MRAG_SAMPLE_STRIDE
+#define MRAG_SAMPLE_STRIDE 16
+#endif
+constexpr int SAMPLE_STRIDE = MRAG_SAMPLE_STRIDE;  // K7 sample pre-pass: every 16th tile of a split (A/B builds: -D)
 
 // |approx - exact| bound for the fp16 scan:
 //   fp16 rounding of both unit vectors: (2u + u^2) * sum|q_i x_i| <= 9.77e-4 (u = 2^-11)
@@ -94,6 +97,32 @@ __device__ __forceinline__ void list_insert(float (&ls)[KL], int (&li)[KL], floa
     li[j] = sw ? cr : tr;
     cs = sw ? ts : cs;
     cr = sw ? tr : cr;
+  }
+}
+
+// The same insertion without the dependent chain: every position compares s with its own
+// old entry (c_j = s > ls[j], monotone in j for a descending list) and takes s, its left
+// neighbour or itself, all from the OLD list. Identical result to list_insert (s equal to an
+// entry goes after it; s <= ls[KL-1] leaves the list unchanged); 3·KL - 2 independent selects
+// per array instead of a KL-deep compare/swap chain (K7's group-test fire path).
+template <int KL>
+__device__ __forceinline__ void list_insert_par(float (&ls)[KL], int (&li)[KL], float s, int r) {
+  bool c[KL];
+#pragma unroll
+  for (int j = 0; j < KL; ++j) c[j] = s > ls[j];
+  float ns[KL];
+  int ni[KL];
+  ns[0] = c[0] ? s : ls[0];
+  ni[0] = c[0] ? r : li[0];
+#pragma unroll
+  for (int j = 1; j < KL; ++j) {
+    ns[j] = c[j] ? (c[j - 1] ? ls[j - 1] : s) : ls[j];
+    ni[j] = c[j] ? (c[j - 1] ? li[j - 1] : r) : li[j];
+  }
+#pragma unroll
+  for (int j = 0; j < KL; ++j) {
+    ls[j] = ns[j];
+    li[j] = ni[j];
   }
 }
 
@@ -571,14 +600,9 @@ __global__ __launch_bounds__(SCAN2_THREADS) void knn_scan3_kernel(ScanParams p) 
       asm volatile("v_max_f32 %0, %0, %1" : "+v"(sm) : "v"(gm));
       smax[qb] = sm;
     } else {
-#ifdef MRAG_K7_ABL_NOINS
-      // timing ablation only (results wrong): no group test ever fires
-      if (__any(gm > thr[qb]) && p.k < 0) {
-#else
       // unlikely: the fire path is laid out away from the k-step's MFMAs, so the common case falls
       // through (no taken branch per k-step) and the two-tile loop keeps ~10 KB of hot code
       if (__builtin_expect(__any(gm > thr[qb]), 0)) {
-#endif
 #ifdef MRAG_K7_STAMPS
         const unsigned long long fire_t0 = __builtin_amdgcn_s_memtime();
 #endif
@@ -586,7 +610,7 @@ __global__ __launch_bounds__(SCAN2_THREADS) void knn_scan3_kernel(ScanParams p) 
         for (int r = 0; r < 4; ++r) {
           const float sv = av[r];
           if (sv > fmaxf(ls[qb][KL3 - 1], theta_f[qb]))
-            list_insert<KL3>(ls[qb], li[qb], sv, prow + 16 * rb + r);
+            list_insert_par<KL3>(ls[qb], li[qb], sv, prow + 16 * rb + r);
         }
         if (may_publish && li[qb][KL3 - 1] >= 0 && ls[qb][KL3 - 1] > published[qb]) {
           published[qb] = ls[qb][KL3 - 1];
@@ -2179,8 +2203,10 @@ int mrag_knn_search(mrag_knn_index* ix, const float* queries, int64_t nq, int32_
   return MRAG_OK;
 }
 
-// Diagnostic (not in mrag.h): the collect-pass bookkeeping of the index's last search, for
-// scripts/knn_collect_diag.py. Valid only while no other search has run on the index since.
+#ifdef MRAG_K7_STAMPS
+// Diagnostic build only (make stamp; not in mrag.h, not in the shipped libmrag.so): the
+// collect-pass bookkeeping of the index's last search, for scripts/knn_collect_diag.py. Valid
+// only while no other search runs on the index: it reads the last search's context buffers.
 // info[8] = S, Qp, cgroups, Sc, ccap, uncertified, overflow flag, KL; fail_list / cand_cnt get
 // the first `uncertified` slots, thresh the first `nthresh` queries (any pointer may be NULL).
 __attribute__((visibility("default"))) int mrag_debug_knn_last_collect(mrag_knn_index* ix, int32_t* info,
@@ -2200,6 +2226,7 @@ __attribute__((visibility("default"))) int mrag_debug_knn_last_collect(mrag_knn_
     MRAG_HIP(hipMemcpy(thresh, c->thresh.p, nthresh * 4, hipMemcpyDeviceToHost));
   return MRAG_OK;
 }
+#endif
 
 int mrag_topk_merge(const double* scores64, const int64_t* rows, int32_t nlists, int64_t nq, int32_t k,
                     float* out_scores, double* out_scores64, int64_t* out_rows, void* stream) {

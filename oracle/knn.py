@@ -14,7 +14,7 @@ exactly in float64 with the semantics pinned in DESIGN.md §3:
 * order (score desc, row asc); at most k rows (fewer if fewer rows match).
 
 Pinned against scikit-learn's brute-force cosine NearestNeighbors in
-``tests/test_oracle_knn.py`` (an independent implementation).
+``tests/test_oracle_pinning.py`` (an independent implementation).
 """
 from __future__ import annotations
 
@@ -103,6 +103,10 @@ def flat_cosine_topk(corpus, labels, queries, k: int, label_filter: int = -1, ro
     cand_r = [[] for _ in range(nq)]
     for c0 in range(0, all_rows.size, chunk):
         rows = all_rows[c0:c0 + chunk]
+        # Residual limit (distinct rows only): the BLAS product rounds a row's f64 score in an
+        # order that can depend on the row's position in the chunk, while the GPU rescoring uses
+        # one fixed order; two DISTINCT rows whose exact scores differ by less than ~1e-16 could
+        # therefore tie-break differently. Bit-identical rows are handled exactly (below).
         cos = cosine_scores(corpus[rows], queries)
         if rep_cos is not None:
             dup = np.nonzero(gid[rows] >= 0)[0]

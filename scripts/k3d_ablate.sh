@@ -1,5 +1,6 @@
 #!/bin/bash
-# K3d timing ablations (results wrong by design): build libs with -DMRAG_K3D_ABL=<mask> (bits in
+# K3d timing ablations (results wrong by design), round 4: run on a checkout of commit 227f50e (the
+# ablation bits were removed from the product kernel in round 5). Builds libs with -DMRAG_K3D_ABL=<mask> (bits in
 # csrc/encoder_kernels.hip; 64 = one reduced value per lane instead of the epilogue stores, the
 # MFMAs kept live) on the CPU side, then (GPU, "run") time the ViT / text GEMM shapes with
 # each. Usage: scripts/k3d_ablate.sh build | run

@@ -5,6 +5,10 @@ Same data as tests/test_knn_gpu.py::test_collect_pass_many_failing_queries (30k 
 different kernels, each compared with the exact oracle. Prints one JSON line per case and, for
 mismatching queries, which rows are missing / extra with their exact scores and scan
 coordinates (tile, main-scan split, collect split).
+
+Needs the diagnostic library (the mrag_debug_knn_last_collect export is not in the shipped one):
+    make -C multimodal-rag-for-image-text-search_amd stamp
+    MRAG_LIB=multimodal-rag-for-image-text-search_amd/lib/libmrag_k7stamp.so python scripts/knn_collect_diag.py
 """
 from __future__ import annotations
 
