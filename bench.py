@@ -324,6 +324,206 @@ def call_pattern_leg(index, q, reps: int = 200):
     return out
 
 
+RETRIEVE_TEXT_DIM = 384
+RETRIEVE_META_ROWS = 1 << 16  # chunk rows in the SQLite catalog per modality (row i -> chunk i mod this)
+
+
+def _sync():
+    import torch
+
+    torch.cuda.synchronize()
+
+
+def _per_call_ms(fn, args_list):
+    """Mean wall ms of fn(*a) over args_list, the device drained before and after."""
+    _sync()
+    t0 = time.perf_counter()
+    for a in args_list:
+        fn(*a)
+    _sync()
+    return (time.perf_counter() - t0) / max(1, len(args_list)) * 1e3
+
+
+def retrieve_pattern_leg(image_index, reps: int = 100):
+    """The reference's per-query path end to end, through the drop-in modules
+    (app/ml/retrieve.py:41-100 with _get_embeddings :120-129): ``retrieve_text(user, query)``
+    = MiniLM on [query] (B = 1) + CLIP-text on the query (B = 1) + ``search_text`` (top-50) over
+    a 1M x 384 table + one SQLite ``get_chunk`` per hit + result dicts; then
+    ``retrieve_images(user, query)`` for the same query = (query embeddings from the cache, as in
+    the reference) + ``search_image`` (top-12) over the 1M x 512 table + lookups. Every query is
+    a distinct string, so the embedding and result caches miss as on fresh queries. Synthetic
+    weights; the tokenisers are the offline ones. The split times each part alone over the same
+    kind of query (wall ms, device drained around each)."""
+    import numpy as np
+    import tempfile
+
+    import torch
+
+    os.environ["MRAG_STORE_PERSIST"] = "0"
+    from app.ml import embeddings as emb_mod
+    from app.ml import retrieve as rmod
+    from app.settings import settings
+    from app.storage.lancedb_store import LanceDBStore
+    from app.storage.schema import MetadataStore
+    from app.vector_store import FlatIndex
+
+    dev = torch.device("cuda", image_index.device if hasattr(image_index, "device") else 0)
+    d = tempfile.mkdtemp(prefix="mrag_bench_retrieve_")
+    store = LanceDBStore(d)
+    g = torch.Generator(device=dev).manual_seed(4000)
+    xt = torch.randn((ROWS_PER_GPU, RETRIEVE_TEXT_DIM), generator=g, device=dev)
+    text_index = FlatIndex(RETRIEVE_TEXT_DIM, device=dev.index or 0)
+    text_index.add(xt)
+    del xt
+    for t, ix, dim, pre in ((store._text_table, text_index, RETRIEVE_TEXT_DIM, "t"),
+                            (store._image_table, image_index, DIM, "i")):
+        t.index, t.dim = ix, dim
+        t.chunk_ids = [f"{pre}{i % RETRIEVE_META_ROWS}" for i in range(ROWS_PER_GPU)]
+        t.metas = ['{"page_no": 1}'] * ROWS_PER_GPU
+        t.labels = {"u0": 0}
+    meta = MetadataStore(os.path.join(d, "metadata.sqlite3"))
+    c = meta._c()
+    for pre, mod in (("t", "text"), ("i", "image")):
+        c.executemany("INSERT INTO chunks VALUES (?,?,?,?,?,?,?,?,?,?)",
+                      ((f"{pre}{i}", f"doc{i >> 8}", mod, f"passage {i} of the synthetic corpus" if mod == "text" else None,
+                        i & 31, None, None, None, "{}", "") for i in range(RETRIEVE_META_ROWS)))
+    c.commit()
+    saved = (rmod._LANCEDB_STORE, rmod._METADATA_STORE)
+    rmod._LANCEDB_STORE, rmod._METADATA_STORE = store, meta
+    words = ["gpu", "vector", "search", "image", "caption", "lecture", "slide", "graph", "diagram", "model",
+             "embedding", "retrieval", "page", "figure", "table", "network", "matrix", "energy", "cell", "river"]
+    rng = np.random.default_rng(5)
+
+    def queries(n, tag):
+        return [f"{tag} {i} " + " ".join(rng.choice(words, 8)) for i in range(n)]
+
+    kt, ki = settings.retrieval.index_topk_text, settings.retrieval.index_topk_image
+    try:
+        for q in queries(10, "warm"):  # model load, first launches, workspace growth
+            rmod.retrieve_text("u0", q)
+            rmod.retrieve_images("u0", q)
+        qs = queries(reps, "q")
+        t_text = _per_call_ms(lambda q: rmod.retrieve_text("u0", q), [(q,) for q in qs])
+        t_img = _per_call_ms(lambda q: rmod.retrieve_images("u0", q), [(q,) for q in qs])
+        hits_t = len(rmod.retrieve_text("u0", qs[0]))
+        hits_i = len(rmod.retrieve_images("u0", qs[0]))
+        # the parts alone (fresh strings: no cache)
+        qs2 = queries(reps, "s")
+        t_minilm = _per_call_ms(lambda q: emb_mod.embed_text_batch([q]), [(q,) for q in qs2])
+        t_clipt = _per_call_ms(lambda q: emb_mod.embed_query_for_images(q), [(q,) for q in qs2])
+        tv = emb_mod.embed_text_batch([qs2[0]])[0].tolist()
+        iv = emb_mod.embed_query_for_images(qs2[0]).tolist()
+        t_st = _per_call_ms(lambda: store.search_text("u0", tv, kt), [()] * reps)
+        t_si = _per_call_ms(lambda: store.search_image("u0", iv, ki), [()] * reps)
+        ids_t = [h["chunk_id"] for h in store.search_text("u0", tv, kt)]
+        t_lk = _per_call_ms(lambda: [meta.get_chunk(cid) for cid in ids_t], [()] * reps)
+    finally:
+        rmod._LANCEDB_STORE, rmod._METADATA_STORE = saved
+        for t in (store._text_table, store._image_table):
+            t.index = None  # the bench owns the image index; the text index is closed here
+        text_index.close()
+        meta.close()
+    return {
+        "retrieve_text_ms": round(t_text, 4),
+        "retrieve_images_ms": round(t_img, 4),
+        "query_pair_ms": round(t_text + t_img, 4),
+        "queries_per_s": round(1e3 / (t_text + t_img), 1),
+        "hits": {"text": hits_t, "image": hits_i},
+        "split_ms": {"minilm_b1_embed_text_batch": round(t_minilm, 4),
+                     "clip_text_b1_embed_query_for_images": round(t_clipt, 4),
+                     f"search_text_top{kt}_1Mx384": round(t_st, 4),
+                     f"search_image_top{ki}_1Mx512": round(t_si, 4),
+                     f"sqlite_get_chunk_x{len(ids_t)}": round(t_lk, 4)},
+        "workload": f"{reps} distinct synthetic queries; text table {ROWS_PER_GPU} x {RETRIEVE_TEXT_DIM}, image table "
+                    f"{ROWS_PER_GPU} x {DIM} (one user), SQLite catalog of {RETRIEVE_META_ROWS} chunks per modality; "
+                    f"top_k text {kt} / image {ki}",
+        "note": "reference call pattern: retrieve_text then retrieve_images per query (retrieve() minus rerank/fusion); "
+                "wall time per call on the host, device drained; split = each part alone",
+    }
+
+
+def _write_images(d: str, n: int, seed: int = 9):
+    """n synthetic photos-like files (3/4 JPEG q90, 1/4 PNG), sizes cycling 640x480 / 800x600 /
+    1024x768 / 480x640: a smooth field + coarse noise upsampled (decodes like natural images,
+    not like white noise)."""
+    import numpy as np
+    from concurrent.futures import ThreadPoolExecutor
+    from PIL import Image
+
+    sizes = [(640, 480), (800, 600), (1024, 768), (480, 640)]
+
+    def one(i):
+        rng = np.random.default_rng((seed, i))
+        w, h = sizes[i % len(sizes)]
+        coarse = rng.integers(0, 256, (h // 16 + 1, w // 16 + 1, 3), dtype=np.uint8)
+        img = Image.fromarray(coarse).resize((w, h), Image.BILINEAR)
+        fine = rng.integers(-4, 5, (h, w, 3))
+        a = np.clip(np.asarray(img, dtype=np.int16) + fine, 0, 255).astype(np.uint8)
+        p = os.path.join(d, f"img{i:05d}.{'png' if i % 4 == 3 else 'jpg'}")
+        Image.fromarray(a).save(p, quality=90) if p.endswith("jpg") else Image.fromarray(a).save(p)
+        return p
+
+    with ThreadPoolExecutor(max_workers=min(16, _usable_cores())) as ex:
+        return list(ex.map(one, range(n)))
+
+
+def ingest_leg(n_images: int = 1024):
+    """``embed_images_batch`` over a folder of image files (app/ml/embeddings.py:73-91, the
+    ingest path behind index_image_nodes): host decode (PIL, thread pool) -> K0 resize + crop on
+    the GPU -> ViT-B/32 -> L2 normalise, batches of 256, the next batch decoded while the GPU works
+    on the current one. Reported: img/s of the whole call and each stage alone over the same
+    files, so the decode share is explicit."""
+    import shutil
+    import tempfile
+
+    import numpy as np
+
+    from app.encoders.preprocess import decode_batch, decode_workers, resize_crop_device
+    from app.ml import embeddings as emb_mod
+
+    d = tempfile.mkdtemp(prefix="mrag_bench_ingest_")
+    try:
+        paths = _write_images(d, n_images)
+        nbytes = sum(os.path.getsize(p) for p in paths)
+        emb_mod.embed_images_batch(paths[:256])  # warm: model + workspaces
+        _sync()
+        t0 = time.perf_counter()
+        out = emb_mod.embed_images_batch(paths)
+        _sync()
+        t_all = time.perf_counter() - t0
+        workers = decode_workers()  # the pool embed_images_batch decodes on (app/encoders/preprocess.py)
+        t0 = time.perf_counter()
+        arrays = decode_batch(paths)
+        t_dec = time.perf_counter() - t0
+        _sync()
+        t0 = time.perf_counter()
+        u8 = [resize_crop_device(arrays[i:i + 256]) for i in range(0, len(arrays), 256)]
+        _sync()
+        t_rs = time.perf_counter() - t0
+        model = emb_mod._ensure_clip()
+        _sync()
+        t0 = time.perf_counter()
+        for b in u8:
+            model.get_image_features(images_u8=b)
+        _sync()
+        t_vit = time.perf_counter() - t0
+        ok = bool(np.allclose(np.linalg.norm(out, axis=1), 1.0, atol=1e-5))
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
+    return {
+        "images_per_s": round(n_images / t_all, 1),
+        "ms_per_256": round(t_all / n_images * 256 * 1e3, 3),
+        "stages_alone_images_per_s": {"host_decode": round(n_images / t_dec, 1),
+                                      "device_resize_crop_incl_h2d": round(n_images / t_rs, 1),
+                                      "vit_b32_tower": round(n_images / t_vit, 1)},
+        "host_decode_share": round(t_dec / t_all, 3),
+        "decode_threads": workers,
+        "unit_rows": ok,
+        "workload": f"{n_images} synthetic files (3/4 JPEG q90, 1/4 PNG; 640x480 .. 1024x768; "
+                    f"{nbytes / 1e6:.1f} MB on disk), embed_images_batch(paths) in batches of 256",
+    }
+
+
 FUSION_ROWS_PER_GPU = 1 << 19  # config 5: 4M text + 4M image rows over 8 GPUs
 FUSION_T = 16                   # synthetic query length (tokens, incl. specials)
 _ORACLE_MODELS = {}
@@ -466,7 +666,9 @@ def fusion_leg(world: int, rank: int, local: int, steps: int, warmup: int):
     # batches runs them. At N > 1 everything stays in one thread: the collectives share one
     # communicator and must be issued in the same order on every rank. MRAG_FUSION_STREAMS=1
     # serialises the branches, MRAG_FUSION_INFLIGHT sets the steps in flight (A/B timing; four
-    # measured +2.8 % over two in five interleaved pairs, profiles/r4s24_fusion_inflight_ab.txt).
+    # measured +4.1 / +1.3 / +2.8 % over two in three interleaved pairs on one box,
+    # profiles/r4s24_fusion_inflight_ab.txt — within the box-to-box spread; re-checked in round 5,
+    # profiles/r5_fusion_inflight_ab.txt).
     two = world == 1 and os.environ.get("MRAG_FUSION_STREAMS", "2") != "1"
     slots = max(1, int(os.environ.get("MRAG_FUSION_INFLIGHT", "4"))) if two else 1
     from concurrent.futures import ThreadPoolExecutor
@@ -582,6 +784,9 @@ def main():
     ap.add_argument("--no-clip", action="store_true")
     ap.add_argument("--no-fusion", action="store_true")
     ap.add_argument("--no-call-pattern", action="store_true")
+    ap.add_argument("--no-retrieve-pattern", action="store_true",
+                    help="skip the per-query retrieve_text / retrieve_images leg")
+    ap.add_argument("--no-ingest", action="store_true", help="skip the embed_images_batch-from-files leg")
     ap.add_argument("--knn-streams", type=int, default=2,
                     help="kNN searches in flight (host threads / streams); 1 = one at a time")
     args = ap.parse_args()
@@ -663,6 +868,33 @@ def main():
     if pool is not None:
         pool.shutdown()
 
+    # N > 1: what the communicator is, which devices the ranks drove, and the collective part of a
+    # step (all-gather of the per-shard (f64 score, row) lists + the K11 merge) timed alone
+    comm = None
+    if world > 1:
+        backend = dist.get_backend()
+        ranks = [None] * world
+        props = torch.cuda.get_device_properties(local)
+        dist.all_gather_object(ranks, {"rank": rank, "local_device": local, "name": props.name,
+                                       "pci_bus": getattr(props, "pci_bus_id", None),
+                                       "host": os.uname().nodename})
+        loc = sharded.search_local(q, TOPK)
+        for _ in range(3):
+            sharded.combine(loc, TOPK)
+        reps = max(10, args.steps)
+        torch.cuda.synchronize()
+        _barrier(world)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            sharded.combine(loc, TOPK)
+        torch.cuda.synchronize()
+        comm_dt = _max_over_ranks(time.perf_counter() - t0, world)
+        comm = {"backend": backend, "collective": "RCCL" if backend == "nccl" else backend,
+                "world": dist.get_world_size(), "devices": ranks,
+                "distinct_devices": len({(r["host"], r["pci_bus"], r["local_device"]) for r in ranks}),
+                "allgather_merge_ms_per_step": round(comm_dt / reps * 1e3, 4),
+                "allgather_bytes_per_rank": NQ * TOPK * 16}
+
     ms_per_step = dt / args.steps * 1e3
     value = world * NQ * args.steps / dt
     avg_scan_s = (scan_ms / max(scan_n, 1)) / 1e3
@@ -686,6 +918,9 @@ def main():
     call_pattern = None
     if world == 1 and not args.no_call_pattern:
         call_pattern = call_pattern_leg(index, q, reps=max(50, 10 * args.steps))
+    if world == 1 and not args.no_retrieve_pattern:
+        call_pattern = call_pattern or {}
+        call_pattern["retrieve"] = retrieve_pattern_leg(index, reps=max(50, 5 * args.steps))
 
     fusion = None
     if not args.no_fusion:  # config 5 (all ranks take part: sharded corpora + all-gathers)
@@ -717,7 +952,8 @@ def main():
                 "dim": DIM,
                 "queries_per_step": NQ,
                 "top_k": TOPK,
-                "parallelism": f"row-sharded x{world}" + (" + RCCL all-gather of per-shard top-k" if world > 1 else ""),
+                "parallelism": f"row-sharded x{world}" + (f" + {comm['collective']} all-gather of per-shard top-k"
+                                                          if comm else ""),
                 "query_vector_pairs_per_s": round(value * ROWS_PER_GPU, 1),
                 "uncertified_queries_last_step": unc,
                 "searches_in_flight": nstreams,
@@ -732,17 +968,25 @@ def main():
                 "unit": "TFLOP/s",
                 "frac": round(achieved_tflops / MFMA_FP16_PEAK_TFLOPS, 4),
                 "traffic": _traffic_from_profiles(),
+                "traffic_source": "profiles/knn_scan_pmc.json: rocprofv3 FETCH_SIZE / WRITE_SIZE passes (separate runs) "
+                                  "of this kernel on the committed tree, 2 x FETCH_SIZE (gfx950) + WRITE_SIZE per launch; "
+                                  "counters cannot be read inside this process",
                 "avg_launch_ms": round(avg_scan_s * 1e3, 4),
                 "algorithmic_flops_per_launch": flops_per_launch,
                 "algorithmic_bytes_per_launch": ROWS_PER_GPU * DIM * 2 + NQ * DIM * 2,
             },
         }
+        if world == 1 and not args.no_ingest:
+            out["call_pattern"] = dict(call_pattern or {}, ingest_embed_images_batch=ingest_leg())
+            call_pattern = out["call_pattern"]
         if not args.no_clip:
             clip = clip_leg(steps=max(30, args.steps), warmup=3)  # single-GPU leg, rank 0; 30+ batches: three in flight reach steady state
             if clip is not None:
                 if not args.no_cpu_baseline:
                     clip["cpu_baseline"] = clip_cpu_baseline()
                 out["clip"] = clip
+        if comm is not None:
+            out["comm"] = comm
         if host_path is not None:
             out["host_buffer_path"] = host_path
         if call_pattern is not None:

@@ -19,7 +19,7 @@ from typing import Optional, Sequence, Tuple
 import numpy as np
 
 from app.encoders import CLIP_TEXT_B32, CLIP_VISION_B32, MINILM_L6, GpuEncoder, load_encoder
-from app.encoders.preprocess import load_batch, load_batch_device
+from app.encoders.preprocess import decode_batch, load_batch, load_batch_device, resize_crop_device
 from app.encoders.tokenize import ClipTokenizer, WordPieceTokenizer
 from app.encoders.weights import encoder_weights, resolve_model_dir, synth_state_dict, synthetic_allowed, SYNTHETIC_ENV
 
@@ -271,6 +271,16 @@ class ClipProcessor:
             ids, mask = self.tokenizer(list(text))
             return BatchInputs(input_ids=ids, attention_mask=mask)
         raise ValueError("ClipProcessor needs images= or text=")
+
+    # The two halves of images= for a caller that pipelines batches (embed_images_batch decodes
+    # batch i + 1 on the host while batch i is resized and encoded on the GPU).
+    @staticmethod
+    def decode(images):
+        return decode_batch(list(images))
+
+    @staticmethod
+    def from_decoded(arrays):
+        return BatchInputs(images_u8=resize_crop_device(arrays, device=_device_index()))
 
 
 class CrossEncoderModel:

@@ -16,6 +16,8 @@ Checked against transformers' CLIPImageProcessor in tests/test_compat_cpu.py.
 """
 from __future__ import annotations
 
+import os
+import threading
 from concurrent.futures import ThreadPoolExecutor
 from pathlib import Path
 from typing import List, Sequence, Union
@@ -24,6 +26,38 @@ import numpy as np
 from PIL import Image
 
 SIZE = 224
+
+
+def decode_workers() -> int:
+    """Host threads for image decode: the cores this process may use (affinity mask, capped by a
+    cgroup CPU quota when one is set — a GPU box lists the whole node's cores), at most 32. PIL
+    releases the GIL inside its decoders, so decode throughput grows with them (the ingest path
+    is decode-bound: DESIGN.md §6)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except Exception:
+        n = os.cpu_count() or 1
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, -(-int(quota) // int(period))))
+    except Exception:
+        pass
+    return max(1, min(32, n))
+
+
+_POOL = None
+_POOL_LOCK = threading.Lock()
+
+
+def _pool() -> ThreadPoolExecutor:
+    """One process-wide decode pool (created on first use, reused by every batch)."""
+    global _POOL
+    with _POOL_LOCK:
+        if _POOL is None:
+            _POOL = ThreadPoolExecutor(max_workers=decode_workers(), thread_name_prefix="mrag-decode")
+        return _POOL
 
 
 def to_u8_224(img: Image.Image, size: int = SIZE) -> np.ndarray:
@@ -107,12 +141,17 @@ def resize_crop_device(arrays: Sequence[np.ndarray], device: int = 0, size: int 
     return out
 
 
-def load_batch_device(items: Sequence[Union[str, Path, Image.Image]], device: int = 0, workers: int = 8):
-    """Decode on a host thread pool, resize + crop on the GPU: u8 [n, 224, 224, 3] CUDA tensor."""
+def decode_batch(items: Sequence[Union[str, Path, Image.Image]]) -> List[np.ndarray]:
+    """Host decode of a batch on the process-wide pool: u8 HxWx3 RGB arrays, in order."""
+    if len(items) == 0:
+        return []
+    return list(_pool().map(decode_rgb, items))
+
+
+def load_batch_device(items: Sequence[Union[str, Path, Image.Image]], device: int = 0):
+    """Decode on the host thread pool, resize + crop on the GPU: u8 [n, 224, 224, 3] CUDA tensor."""
     if len(items) == 0:
         import torch
 
         return torch.empty((0, SIZE, SIZE, 3), dtype=torch.uint8, device=torch.device("cuda", device))
-    with ThreadPoolExecutor(max_workers=max(1, min(workers, len(items)))) as ex:
-        arrays = list(ex.map(decode_rgb, items))
-    return resize_crop_device(arrays, device=device)
+    return resize_crop_device(decode_batch(items), device=device)

@@ -15,6 +15,7 @@ image batch is max(batch_size, 256) (results do not depend on it).
 """
 from __future__ import annotations
 
+import os
 from pathlib import Path
 from typing import Any, List, Mapping, Optional, Sequence
 
@@ -106,6 +107,20 @@ def embed_images_batch(paths: Sequence[Path], batch_size: int = 8) -> np.ndarray
     step = max(batch_size, 256) if native else batch_size
     paths = list(paths)
     out: List[np.ndarray] = []
+    if native and os.environ.get("MRAG_HOST_RESIZE") != "1":
+        # decode-bound ingest: the host decodes batch i + 1 while the GPU resizes and encodes batch i
+        from concurrent.futures import ThreadPoolExecutor
+
+        starts = list(range(0, len(paths), step))
+        with ThreadPoolExecutor(max_workers=1) as ahead:
+            nxt = ahead.submit(processor.decode, paths[0:step])
+            for i, start in enumerate(starts):
+                arrays = nxt.result()
+                if i + 1 < len(starts):
+                    nxt = ahead.submit(processor.decode, paths[starts[i + 1]:starts[i + 1] + step])
+                inputs = processor.from_decoded(arrays)
+                out.append(_to_numpy(model.get_image_features(**_kwargs(inputs))))
+        return _normalize(np.vstack(out))
     for start in range(0, len(paths), step):
         batch_paths = paths[start:start + step]
         if native:

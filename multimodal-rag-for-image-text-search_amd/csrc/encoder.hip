@@ -78,6 +78,14 @@ struct mrag_encoder {
   hipEvent_t done = nullptr;
   hipStream_t last_stream = nullptr;
   hipEvent_t null_ev = nullptr;  // device inputs on the NULL stream: the call waits for it
+  // Small host-pointer token batches (the reference's one query per retrieve call) replay a
+  // captured hipGraph of the forward instead of ~90 individual launches; keyed by shape, valid
+  // while the workspace buffers it baked in keep their addresses (`sig`).
+  struct Graph {
+    hipGraphExec_t exec = nullptr;
+    std::vector<const void*> sig;
+  };
+  std::map<uint64_t, Graph> graphs;
 };
 
 namespace {
@@ -383,6 +391,44 @@ int check_ready(mrag_encoder* e) {
 
 }  // namespace
 
+namespace {
+// Run `forward` on s as a replay of its captured graph (captured on first use of this shape, or
+// again when a buffer it baked in moved). The kernels and their order are exactly those of a
+// direct call, so results are bit-identical to it (tests/test_encoders_gpu.py).
+template <class F>
+int run_graph(mrag_encoder* e, uint64_t key, std::vector<const void*> sig, hipStream_t s, F&& forward) {
+  auto it = e->graphs.find(key);
+  if (it != e->graphs.end() && it->second.sig != sig) {
+    (void)hipGraphExecDestroy(it->second.exec);
+    e->graphs.erase(it);
+    it = e->graphs.end();
+  }
+  if (it == e->graphs.end()) {
+    if (e->graphs.size() >= 128) {  // bounded cache: query lengths vary
+      for (auto& kv : e->graphs) (void)hipGraphExecDestroy(kv.second.exec);
+      e->graphs.clear();
+    }
+    hipGraph_t gr = nullptr;
+    MRAG_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+    const int rc = forward(s);
+    const hipError_t ce = hipStreamEndCapture(s, &gr);
+    if (rc != MRAG_OK) {
+      if (gr) (void)hipGraphDestroy(gr);
+      return rc;
+    }
+    if (ce != hipSuccess) return mrag::fail(MRAG_ERR_HIP, "graph capture: %s", hipGetErrorString(ce));
+    hipGraphExec_t ex = nullptr;
+    const hipError_t ie = hipGraphInstantiate(&ex, gr, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(gr);
+    if (ie != hipSuccess) return mrag::fail(MRAG_ERR_HIP, "graph instantiate: %s", hipGetErrorString(ie));
+    it = e->graphs.emplace(key, mrag_encoder::Graph{ex, std::move(sig)}).first;
+  }
+  MRAG_HIP(hipGraphLaunch(it->second.exec, s));
+  return MRAG_OK;
+}
+
+}  // namespace
+
 extern "C" {
 
 int mrag_encoder_create(const mrag_encoder_config* cfg, int32_t device, mrag_encoder** out) {
@@ -435,6 +481,8 @@ int mrag_encoder_destroy(mrag_encoder* e) {
     if (e->last_stream) (void)hipEventSynchronize(e->done);
     if (e->done) (void)hipEventDestroy(e->done);
     if (e->null_ev) (void)hipEventDestroy(e->null_ev);
+    for (auto& kv : e->graphs) (void)hipGraphExecDestroy(kv.second.exec);
+    e->graphs.clear();
     for (auto& L : e->layers)
       for (Buf* b : {&L.wqkv, &L.bqkv, &L.wo, &L.bo, &L.w1, &L.b1, &L.w2, &L.b2, &L.ln1g, &L.ln1b, &L.ln2g, &L.ln2b})
         buf_free(*b);
@@ -454,6 +502,8 @@ int mrag_encoder_set_param(mrag_encoder* e, const char* cname, const float* data
   std::lock_guard<std::mutex> lk(e->mu);
   mrag::DeviceGuard g(e->device);
   if (e->last_stream) MRAG_HIP(hipEventSynchronize(e->done));  // a forward may still read the weights
+  for (auto& kv : e->graphs) (void)hipGraphExecDestroy(kv.second.exec);  // recaptured on next use
+  e->graphs.clear();
   const std::string name(cname);
   const auto& c = e->cfg;
   bool known = false;
@@ -660,34 +710,47 @@ int mrag_encoder_embed_tokens(mrag_encoder* e, const int32_t* ids, const int32_t
     if (int rc = buf_ensure(e->OUT, (size_t)B * outD * 4)) return rc;
     dst = (float*)e->OUT.p;
   }
-  if (c.kind == MRAG_ENC_CLIP_TEXT) {
-    if (int rc = launch_token_embed(dids, (const float*)e->tok.p, (const float*)e->pos.p, nullptr, nullptr, X, B, T, D,
-                                    c.vocab, s))
-      return rc;
-    if (int rc = launch_eos_rows(dids, B, T, c.eos_token_id, (int*)e->ROWS.p, s)) return rc;
-    const bool prune = c.layers > 0;
-    for (int i = 0; i < c.layers; ++i) {
-      if (prune && i == c.layers - 1) {
-        if (int rc = clip_layer_pooled(e, e->layers[i], B, T, dmask, 1, (const int*)e->ROWS.p, s)) return rc;
-      } else if (int rc = clip_layer(e, e->layers[i], B, T, dmask, 1, s)) {
+  auto forward = [&](hipStream_t s) -> int {
+    if (c.kind == MRAG_ENC_CLIP_TEXT) {
+      if (int rc = launch_token_embed(dids, (const float*)e->tok.p, (const float*)e->pos.p, nullptr, nullptr, X, B, T,
+                                      D, c.vocab, s))
         return rc;
+      if (int rc = launch_eos_rows(dids, B, T, c.eos_token_id, (int*)e->ROWS.p, s)) return rc;
+      const bool prune = c.layers > 0;
+      for (int i = 0; i < c.layers; ++i) {
+        if (prune && i == c.layers - 1) {
+          if (int rc = clip_layer_pooled(e, e->layers[i], B, T, dmask, 1, (const int*)e->ROWS.p, s)) return rc;
+        } else if (int rc = clip_layer(e, e->layers[i], B, T, dmask, 1, s)) {
+          return rc;
+        }
       }
+      if (int rc = layernorm(prune ? (const float*)e->XG.p : X, prune ? nullptr : (const int*)e->ROWS.p, nullptr,
+                             (_Float16*)e->POOL16.p, e->post_g, e->post_b, B, D, c.ln_eps, s))
+        return rc;
+      if (int rc = gemm(e->POOL16.p, e->proj_w.p, nullptr, dst, B, c.proj_dim, D, c.proj_dim, EPI_F32, s)) return rc;
+    } else {
+      if (int rc = launch_token_embed(dids, (const float*)e->tok.p, (const float*)e->pos.p, (const float*)e->type0.p,
+                                      nullptr, X, B, T, D, c.vocab, s))
+        return rc;
+      if (int rc = layernorm(X, nullptr, X, H, e->emb_g, e->emb_b, B * T, D, c.ln_eps, s)) return rc;
+      for (int i = 0; i < c.layers; ++i)
+        if (int rc = bert_layer(e, e->layers[i], B, T, dmask, s)) return rc;
+      if (int rc = launch_mean_pool(X, dmask, dst, B, T, D, s)) return rc;
     }
-    if (int rc = layernorm(prune ? (const float*)e->XG.p : X, prune ? nullptr : (const int*)e->ROWS.p, nullptr,
-                           (_Float16*)e->POOL16.p, e->post_g, e->post_b, B, D, c.ln_eps, s))
-      return rc;
-    if (int rc = gemm(e->POOL16.p, e->proj_w.p, nullptr, dst, B, c.proj_dim, D, c.proj_dim, EPI_F32, s)) return rc;
-  } else {
-    if (int rc = launch_token_embed(dids, (const float*)e->tok.p, (const float*)e->pos.p, (const float*)e->type0.p,
-                                    nullptr, X, B, T, D, c.vocab, s))
-      return rc;
-    if (int rc = layernorm(X, nullptr, X, H, e->emb_g, e->emb_b, B * T, D, c.ln_eps, s)) return rc;
-    for (int i = 0; i < c.layers; ++i)
-      if (int rc = bert_layer(e, e->layers[i], B, T, dmask, s)) return rc;
-    if (int rc = launch_mean_pool(X, dmask, dst, B, T, D, s)) return rc;
+    if (normalize)
+      if (int rc = mrag_l2norm_rows(dst, dst, B, outD, s)) return rc;
+    return MRAG_OK;
+  };
+  // host-pointer calls of up to 2048 tokens (every input and output then lives in this handle's
+  // workspace, at addresses the graph can bake in): graph replay; otherwise direct launches
+  if (ptr_kind == MRAG_PTR_HOST && (int64_t)B * T <= 2048) {
+    const uint64_t key = ((uint64_t)B << 32) | ((uint64_t)T << 2) | (dmask ? 2u : 0u) | (normalize ? 1u : 0u);
+    std::vector<const void*> sig = {e->X.p,  e->H16.p, e->QKV.p, e->ATT.p,    e->F16.p, e->XG.p, e->AG.p,
+                                    e->HG.p, e->FG.p,  e->ROWS.p, e->POOL16.p, e->IDS.p, e->MASK.p, e->OUT.p};
+    if (int rc = run_graph(e, key, std::move(sig), s, forward)) return rc;
+  } else if (int rc = forward(s)) {
+    return rc;
   }
-  if (normalize)
-    if (int rc = mrag_l2norm_rows(dst, dst, B, outD, s)) return rc;
   if (ptr_kind == MRAG_PTR_HOST) MRAG_HIP(hipMemcpyAsync(out, dst, (size_t)B * outD * 4, hipMemcpyDeviceToHost, s));
   drain.armed = false;
   return end_call(e, s, ptr_kind, stream_arg);

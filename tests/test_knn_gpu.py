@@ -232,6 +232,30 @@ def test_seeded_threshold_prepass(cuda, label_filter):
         _check(s, r, os_, or_)
 
 
+@pytest.mark.parametrize("dim", [128, 512])
+def test_k7_to_16_between_publish_and_deep_lists(cuda, dim):
+    """6 < k <= 16 on 256-query workgroups: above the per-lane list depth (no lane publishes its
+    6th, the seed is the only shared bound) and below the sample stride switch. Clustered rows
+    with exact duplicates and near-duplicate queries put the seed right at the k-th score; k = 7,
+    12, 16, with and without a label prefilter: exact results. (Written for the round-5 class
+    bound, which was measured no faster and not kept: notes/knn_scan_experiments.md.)"""
+    from app.vector_store import FlatIndex
+
+    n = 270_000 if dim == 128 else 140_000
+    x = clustered_corpus(n, dim, 41, n_clusters=64, spread=0.05, dup_frac=0.1)
+    lab = labels_for(len(x), 3, 42)
+    rng = np.random.default_rng(43)
+    q = np.concatenate([x[rng.integers(0, len(x), 600)] + 0.005 * rng.standard_normal((600, dim)).astype(np.float32),
+                        rng.standard_normal((424, dim)).astype(np.float32)])
+    ix = FlatIndex(dim)
+    ix.add(x, lab)
+    for k in (7, 12, 16):
+        for f in (-1, 1):
+            s, r = ix.search(q, k, label=f)
+            os_, or_ = flat_cosine_topk(x, lab, q, k, label_filter=f)
+            _check(s, r, os_, or_)
+
+
 @pytest.mark.parametrize("dim", [384, 512])
 def test_small_tables_k_above_list_depth(cuda, dim):
     """Tables of a few tiles with k above the per-split list depth (the reference's
