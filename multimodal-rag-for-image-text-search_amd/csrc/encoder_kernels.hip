@@ -30,6 +30,35 @@ __device__ __forceinline__ void glds_x4(const void* gsrc, uint32_t lds_addr) {
       : "memory");
 }
 
+#define MRAG_VMCNT_CASE(n) \
+  case n: asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory"); break;
+__device__ __forceinline__ void vmcnt_wait(int n) {  // n wave-uniform, 0..63
+  switch (n) {
+    MRAG_VMCNT_CASE(1) MRAG_VMCNT_CASE(2) MRAG_VMCNT_CASE(3) MRAG_VMCNT_CASE(4) MRAG_VMCNT_CASE(5)
+    MRAG_VMCNT_CASE(6) MRAG_VMCNT_CASE(7) MRAG_VMCNT_CASE(8) MRAG_VMCNT_CASE(9) MRAG_VMCNT_CASE(10)
+    MRAG_VMCNT_CASE(11) MRAG_VMCNT_CASE(12) MRAG_VMCNT_CASE(13) MRAG_VMCNT_CASE(14) MRAG_VMCNT_CASE(15)
+    MRAG_VMCNT_CASE(16) MRAG_VMCNT_CASE(17) MRAG_VMCNT_CASE(18) MRAG_VMCNT_CASE(19) MRAG_VMCNT_CASE(20)
+    MRAG_VMCNT_CASE(21) MRAG_VMCNT_CASE(22) MRAG_VMCNT_CASE(23) MRAG_VMCNT_CASE(24) MRAG_VMCNT_CASE(25)
+    MRAG_VMCNT_CASE(26) MRAG_VMCNT_CASE(27) MRAG_VMCNT_CASE(28) MRAG_VMCNT_CASE(29) MRAG_VMCNT_CASE(30)
+    MRAG_VMCNT_CASE(31) MRAG_VMCNT_CASE(32) MRAG_VMCNT_CASE(33) MRAG_VMCNT_CASE(34) MRAG_VMCNT_CASE(35)
+    MRAG_VMCNT_CASE(36) MRAG_VMCNT_CASE(37) MRAG_VMCNT_CASE(38) MRAG_VMCNT_CASE(39) MRAG_VMCNT_CASE(40)
+    MRAG_VMCNT_CASE(41) MRAG_VMCNT_CASE(42) MRAG_VMCNT_CASE(43) MRAG_VMCNT_CASE(44) MRAG_VMCNT_CASE(45)
+    MRAG_VMCNT_CASE(46) MRAG_VMCNT_CASE(47) MRAG_VMCNT_CASE(48) MRAG_VMCNT_CASE(49) MRAG_VMCNT_CASE(50)
+    MRAG_VMCNT_CASE(51) MRAG_VMCNT_CASE(52) MRAG_VMCNT_CASE(53) MRAG_VMCNT_CASE(54) MRAG_VMCNT_CASE(55)
+    MRAG_VMCNT_CASE(56) MRAG_VMCNT_CASE(57) MRAG_VMCNT_CASE(58) MRAG_VMCNT_CASE(59) MRAG_VMCNT_CASE(60)
+    MRAG_VMCNT_CASE(61) MRAG_VMCNT_CASE(62) MRAG_VMCNT_CASE(63)
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
+}
+#undef MRAG_VMCNT_CASE
+// compile-time count: one s_waitcnt, never merged with the dynamic ladder above (which the
+// compiler lowers to a compare/branch tree of ~20 scalar instructions per call)
+template <int N>
+__device__ __forceinline__ void vmcnt_wait_c() {
+  static_assert(N >= 0 && N < 64, "vmcnt field is 6 bits");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
 // ---------------------------------------------------------------------------
 // K3: C[m][n] (+)= act(sum_k A[m][k] W[n][k] + bias[n])   (the "NT" GEMM of nn.Linear)
 //
@@ -277,6 +306,122 @@ __global__ __launch_bounds__(GTHREADS) void gemm_nt_kernel(GemmArgs g) {
 }
 
 // ---------------------------------------------------------------------------
+// K3s (M <= 64: one query per retrieve call, a single image): one wave per 16 output columns,
+// so a GEMM spreads its weight stream over N / 16 CUs instead of K3's N / 128 workgroups (at
+// M = 12 K3's residual GEMMs ran 12-15 us on 3-4 workgroups, each streaming 128 weight rows).
+// An element's order is K3's: one accumulator, 32-deep MFMA 16x16x32 chunks in ascending k,
+// the weight fragment as operand A, and the same epilogue, so a row's embedding does not depend
+// on its batch size (tests/test_encoders_gpu.py batch-vs-alone tests).
+// The wave streams k-pairs (64 k: 16 weight rows + 16 MB activation rows, 1 KiB LDS-DMA per
+// 8 rows) through a ring of RP pairs in LDS, all LDS-DMA (no VGPRs held by loads in flight); a
+// load lane takes row lane >> 3 and 16-byte chunk (lane & 7) ^ (lane >> 3) of its 8 rows (whole
+// 128-byte lines per 8 lanes), so the fragment reads (8 rows of one chunk per 8 lanes) are
+// bank-conflict free. The next pair's fragments are read before this pair's MFMAs.
+template <int MB>
+struct SkinnyGeom {
+  static constexpr int PER = 2 + 2 * MB;                            // 1 KiB pieces per k-pair
+  static constexpr int RP = MB == 1 ? 16 : (MB == 2 ? 10 : (MB == 3 ? 7 : 6));  // (RP - 1) PER < 64
+  static constexpr int LDS = RP * PER * 1024;
+  static_assert((RP - 1) * PER < 64, "vmcnt field");
+};
+
+template <int EPI, int MB>
+__global__ __launch_bounds__(64) void gemm_skinny_kernel(GemmArgs g) {
+  using G = SkinnyGeom<MB>;
+  constexpr int PER = G::PER, RP = G::RP;
+  __shared__ __attribute__((aligned(16))) char smem[G::LDS];
+  const int lane = threadIdx.x;
+  const uint32_t lds_base = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)((AS3 char*)smem));
+  const int n0 = blockIdx.x * 16;
+  const int npairs = g.K / 64;
+
+  // load side: piece j of a pair = rows 8 (j & 1) .. + 8 of the weight block (j < 2) or of
+  // activation block (j - 2) >> 1
+  const int lr = lane >> 3, lc = (lane & 7) ^ (lane >> 3);
+  const _Float16* src[PER];
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int row = 8 * (j & 1) + lr;
+    if (j < 2) {
+      src[j] = g.W + (size_t)(n0 + row) * g.ldw + lc * 8;
+    } else {
+      const int m = min(16 * ((j - 2) >> 1) + row, g.M - 1);
+      src[j] = g.A + (size_t)m * g.lda + lc * 8;
+    }
+  }
+  auto issue = [&](int p) {
+    const uint32_t slot = lds_base + (uint32_t)((p % RP) * PER * 1024);
+#pragma unroll
+    for (int j = 0; j < PER; ++j) glds_x4(src[j] + p * 64, slot + j * 1024);
+  };
+  // read side: lane L holds row r = L & 15, chunk 4 q + (L >> 4) of k-step q of the pair
+  const int r = lane & 15, r7 = r & 7;
+  int offq[2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) offq[q] = (r >> 3) * 1024 + (r7 * 8 + ((4 * q + (lane >> 4)) ^ r7)) * 16;
+
+  half8 wf[2][2], af[2][MB][2];  // [register set][..][k-step q]
+  auto read = [&](auto set_c, int p) {
+    constexpr int S = decltype(set_c)::value;
+    const char* slot = (const char*)smem + (p % RP) * PER * 1024;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      wf[S][q] = *(const half8*)(slot + offq[q]);
+#pragma unroll
+      for (int b = 0; b < MB; ++b) af[S][b][q] = *(const half8*)(slot + (2 + 2 * b) * 1024 + offq[q]);
+    }
+  };
+  // pair p + 1 landed (pairs up to p + RP issued): the younger ones may stay in flight
+  auto wait_next = [&](int p) {
+    if (p + RP + 1 <= npairs) vmcnt_wait_c<(RP - 1) * PER>();
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
+
+  f32x4 acc[MB];
+#pragma unroll
+  for (int b = 0; b < MB; ++b) acc[b] = f32x4{};
+  const int pro = min(RP, npairs);
+  for (int p = 0; p < pro; ++p) issue(p);
+  if (RP < npairs) vmcnt_wait_c<(RP - 1) * PER>();
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  read(std::integral_constant<int, 0>{}, 0);
+
+  // step p: pair p's fragments (read a step ago) are in registers once their reads return, so its
+  // slot is refilled with pair p + RP first; then pair p + 1's fragments are read under pair
+  // p's MFMAs
+  auto step = [&](auto set_c, int p) {
+    constexpr int S = decltype(set_c)::value;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (p + RP < npairs) issue(p + RP);
+    if (p + 1 < npairs) wait_next(p);
+    // unconditional (at p + 1 == npairs it reads a stale slot, never used), so that the MFMAs
+    // below wait only for this set's reads on every path
+    read(std::integral_constant<int, 1 - S>{}, p + 1);
+    __builtin_amdgcn_sched_barrier(0);  // the reads go out before the MFMAs
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int b = 0; b < MB; ++b) acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[S][q], af[S][b][q], acc[b], 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  for (int p = 0; p < npairs; p += 2) {
+    step(std::integral_constant<int, 0>{}, p);
+    if (p + 1 < npairs) step(std::integral_constant<int, 1>{}, p + 1);
+  }
+
+  // epilogue (K3's): lane holds C[m = 16 b + r][n0 + 4 (lane >> 4) + 0..3]
+  const int n = n0 + 4 * (lane >> 4);
+  f32x4 bv = f32x4{};
+  if (g.bias) bv = *(const f32x4*)(g.bias + n);
+  const float bn[4] = {bv[0], bv[1], bv[2], bv[3]};
+#pragma unroll
+  for (int b = 0; b < MB; ++b) {
+    const int m = 16 * b + r;
+    if (m < g.M) gemm_store4<EPI>(g, m, n, acc[b], bn);
+  }
+}
+
+// ---------------------------------------------------------------------------
 // K3d (M >= 1024, N % 256 == 0: the ViT batches): persistent, one workgroup per CU, 256 x 256
 // x 64 tiles, 8 waves (2 M x 4 N, 128 x 64 each), an eight-phase pipeline whose LDS-DMA
 // prefetch stays in flight across barriers and across tiles, two wave groups in ping-pong.
@@ -332,34 +477,6 @@ __device__ __forceinline__ int g8_colperm(int jj) {
   return 8 * f + 4 * jb + r;
 }
 
-#define MRAG_VMCNT_CASE(n) \
-  case n: asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory"); break;
-__device__ __forceinline__ void vmcnt_wait(int n) {  // n wave-uniform, 0..63
-  switch (n) {
-    MRAG_VMCNT_CASE(1) MRAG_VMCNT_CASE(2) MRAG_VMCNT_CASE(3) MRAG_VMCNT_CASE(4) MRAG_VMCNT_CASE(5)
-    MRAG_VMCNT_CASE(6) MRAG_VMCNT_CASE(7) MRAG_VMCNT_CASE(8) MRAG_VMCNT_CASE(9) MRAG_VMCNT_CASE(10)
-    MRAG_VMCNT_CASE(11) MRAG_VMCNT_CASE(12) MRAG_VMCNT_CASE(13) MRAG_VMCNT_CASE(14) MRAG_VMCNT_CASE(15)
-    MRAG_VMCNT_CASE(16) MRAG_VMCNT_CASE(17) MRAG_VMCNT_CASE(18) MRAG_VMCNT_CASE(19) MRAG_VMCNT_CASE(20)
-    MRAG_VMCNT_CASE(21) MRAG_VMCNT_CASE(22) MRAG_VMCNT_CASE(23) MRAG_VMCNT_CASE(24) MRAG_VMCNT_CASE(25)
-    MRAG_VMCNT_CASE(26) MRAG_VMCNT_CASE(27) MRAG_VMCNT_CASE(28) MRAG_VMCNT_CASE(29) MRAG_VMCNT_CASE(30)
-    MRAG_VMCNT_CASE(31) MRAG_VMCNT_CASE(32) MRAG_VMCNT_CASE(33) MRAG_VMCNT_CASE(34) MRAG_VMCNT_CASE(35)
-    MRAG_VMCNT_CASE(36) MRAG_VMCNT_CASE(37) MRAG_VMCNT_CASE(38) MRAG_VMCNT_CASE(39) MRAG_VMCNT_CASE(40)
-    MRAG_VMCNT_CASE(41) MRAG_VMCNT_CASE(42) MRAG_VMCNT_CASE(43) MRAG_VMCNT_CASE(44) MRAG_VMCNT_CASE(45)
-    MRAG_VMCNT_CASE(46) MRAG_VMCNT_CASE(47) MRAG_VMCNT_CASE(48) MRAG_VMCNT_CASE(49) MRAG_VMCNT_CASE(50)
-    MRAG_VMCNT_CASE(51) MRAG_VMCNT_CASE(52) MRAG_VMCNT_CASE(53) MRAG_VMCNT_CASE(54) MRAG_VMCNT_CASE(55)
-    MRAG_VMCNT_CASE(56) MRAG_VMCNT_CASE(57) MRAG_VMCNT_CASE(58) MRAG_VMCNT_CASE(59) MRAG_VMCNT_CASE(60)
-    MRAG_VMCNT_CASE(61) MRAG_VMCNT_CASE(62) MRAG_VMCNT_CASE(63)
-    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-  }
-}
-#undef MRAG_VMCNT_CASE
-// compile-time count: one s_waitcnt, never merged with the dynamic ladder above (which the
-// compiler lowers to a compare/branch tree of ~20 scalar instructions per call)
-template <int N>
-__device__ __forceinline__ void vmcnt_wait_c() {
-  static_assert(N >= 0 && N < 64, "vmcnt field is 6 bits");
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
 
 template <int EPI>
 __global__ __launch_bounds__(G8_THREADS) void gemm_8p_kernel(GemmArgs g) {
@@ -1269,6 +1386,13 @@ template <int EPI>
 struct K3Kern {
   static constexpr auto fn = gemm_nt_kernel<EPI>;
 };
+template <int MB>
+struct K3sKern {
+  template <int EPI>
+  struct Kern {
+    static constexpr auto fn = gemm_skinny_kernel<EPI, MB>;
+  };
+};
 
 int launch_gemm(const GemmArgs& g, int epi, hipStream_t s) {
   if (g.M <= 0) return MRAG_OK;
@@ -1280,6 +1404,15 @@ int launch_gemm(const GemmArgs& g, int epi, hipStream_t s) {
     const int ntiles = ((g.M + G8Geom::BM - 1) / G8Geom::BM) * (g.N / G8Geom::BN);
     const int nb = std::min((ntiles + 7) / 8 * 8, std::max(8, num_cus() / 8 * 8));
     return launch_epi<K3dKern>(epi, dim3((unsigned)nb), dim3(G8_THREADS), s, g);
+  }
+  if (g.M <= 64) {
+    const dim3 grid((unsigned)(g.N / 16));
+    switch ((g.M + 15) / 16) {
+      case 1: return launch_epi<K3sKern<1>::Kern>(epi, grid, dim3(64), s, g);
+      case 2: return launch_epi<K3sKern<2>::Kern>(epi, grid, dim3(64), s, g);
+      case 3: return launch_epi<K3sKern<3>::Kern>(epi, grid, dim3(64), s, g);
+      default: return launch_epi<K3sKern<4>::Kern>(epi, grid, dim3(64), s, g);
+    }
   }
   const dim3 grid((unsigned)(((g.M + GM - 1) / GM) * (g.N / GN)));
   return launch_epi<K3Kern>(epi, grid, dim3(GTHREADS), s, g);

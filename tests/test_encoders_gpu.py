@@ -230,6 +230,52 @@ def test_gemm_shapes_every_epilogue(cuda):
             assert err < (2e-3 if epi <= 2 else 2e-5), (M, N, K, epi, err)
 
 
+@pytest.mark.parametrize("N,K", [(384, 384), (384, 1536), (1152, 384), (1536, 384), (512, 2048), (2048, 512),
+                                 (768, 3072), (2304, 768), (128, 64), (256, 128)])
+def test_gemm_skinny_rows_equal_k3(cuda, N, K):
+    """K3s (M <= 64: one query / one image per call) against K3 on the same rows: every epilogue,
+    M = 1, 5, 16, 17, 33, 50, 64 (1-4 activation blocks, ragged), bit-identical to rows 0..M-1 of
+    a 200-row K3 call over the same A rows (so a query's embedding does not depend on its batch
+    size), and within the K3 tolerance of a torch fp32 product; K from 64 (one k-pair, no ring
+    wrap) to 3072 (the ring wraps several times)."""
+    import torch
+
+    from app.encoders import gemm_nt
+
+    g = torch.Generator(device=cuda).manual_seed(N + K)
+    Mb = 200
+    A = (torch.randn(Mb, K, generator=g, device=cuda) * 0.5).half()
+    W = (torch.randn(N, K, generator=g, device=cuda) * 0.05).half()
+    bias = torch.randn(N, generator=g, device=cuda) * 0.1
+    C0 = torch.randn(Mb, N, generator=g, device=cuda)
+    for epi in range(5):
+        def run(M):
+            if epi <= 2:
+                C = torch.full((M, N), float("nan"), dtype=torch.float16, device=cuda)
+            elif epi == 3:
+                C = C0[:M].clone()
+            else:
+                C = torch.full((M, N), float("nan"), dtype=torch.float32, device=cuda)
+            gemm_nt(A[:M].contiguous(), W, bias, C, epi)
+            return C
+
+        big = run(Mb)
+        ref = A.float() @ W.float().t() + bias
+        if epi == 1:
+            ref = ref * torch.sigmoid(1.702 * ref)
+        elif epi == 2:
+            ref = torch.nn.functional.gelu(ref)
+        if epi == 3:
+            ref = ref + C0
+        for M in (1, 5, 16, 17, 33, 50, 64):
+            C = run(M)
+            torch.cuda.synchronize()
+            assert not torch.isnan(C.float()).any(), (M, epi)
+            assert torch.equal(C, big[:M]), ("skinny != K3 rows", M, N, K, epi)
+            err = (C.float() - ref[:M]).abs().max().item() / ref[:M].abs().max().item()
+            assert err < (2e-3 if epi <= 2 else 2e-5), (M, N, K, epi, err)
+
+
 def test_gelu_erf_epilogue_sweep(cuda):
     """the erf-GELU epilogue (A&S 7.1.26 + hardware rcp/exp2) swept over x in
     [-8, 8) against torch.nn.functional.gelu (exact erf) on the fp16 output, with an absolute
