@@ -10,6 +10,7 @@
 // matrix, f32 biases / LayerNorm params / embeddings. A forward is ~7 launches per layer
 // on one HIP stream; activations live in a per-handle workspace sized for the largest
 // batch seen.
+#include <algorithm>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -55,6 +56,20 @@ __global__ void f32_to_f16_kernel(const float* __restrict__ in, _Float16* __rest
 
 }  // namespace
 
+// One forward's activations. A large image batch runs as MRAG_IMG_LANES sub-batches ("lanes"),
+// each on its own workspace and stream (see mrag_encoder_embed_images).
+#ifndef MRAG_IMG_LANES
+#define MRAG_IMG_LANES 2
+#endif
+#ifndef MRAG_IMG_LANE_MIN
+#define MRAG_IMG_LANE_MIN 128
+#endif
+struct Work {
+  Buf X, H16, QKV, ATT, F16, PATCH, IMG, IDS, MASK, TYPES, ROWS, POOL16, OUT, POOL32;
+  Buf XG, AG, HG, FG;  // the pooled rows of a CLIP tower's last layer (clip_layer_pooled)
+  int64_t ws_tokens = 0, ws_batch = 0;
+};
+
 struct mrag_encoder {
   std::mutex mu;
   mrag_encoder_config cfg;
@@ -64,13 +79,15 @@ struct mrag_encoder {
   // embeddings / heads
   Buf patch_w, cls, pos, pre_g, pre_b, post_g, post_b, proj_w;  // vision
   Buf tok, type0, emb_g, emb_b;                                  // text / bert (+pos); type0 = [2][D]
-  Buf pool_w, pool_b, cls_w, cls_b, POOL32;                      // bert pair: pooler + classifier
+  Buf pool_w, pool_b, cls_w, cls_b;                              // bert pair: pooler + classifier
   std::map<std::string, bool> loaded;
   std::vector<std::string> expected;
-  // workspace
-  Buf X, H16, QKV, ATT, F16, PATCH, IMG, IDS, MASK, TYPES, ROWS, POOL16, OUT;
-  Buf XG, AG, HG, FG;  // the pooled rows of a CLIP tower's last layer (clip_layer_pooled)
-  int64_t ws_tokens = 0, ws_batch = 0;
+  // workspace of a forward: w points at work[0], or at work[i] while image lane i is enqueued
+  Work work[MRAG_IMG_LANES];
+  Work* w = &work[0];
+  // image lanes 1.. (mrag_encoder_embed_images): their streams and the fork / join events
+  hipStream_t lane_stream[MRAG_IMG_LANES] = {};
+  hipEvent_t lane_ev[MRAG_IMG_LANES] = {};
   // Device-pointer calls return without a host sync (stream-ordered, like any kernel launch):
   // `done` marks the end of the last call's work on `last_stream`; a call on another stream
   // first waits for it (the workspace is shared), and a workspace reallocation first
@@ -89,6 +106,20 @@ struct mrag_encoder {
 };
 
 namespace {
+
+// Image handles of the process, for the lane decision of mrag_encoder_embed_images: a handle
+// that is the only image handle on its device cannot have image calls of other handles beside
+// its own. (Asking the runtime whether another handle's last call is still running — an event
+// query per call — cost 4-5 % of the three-batches-in-flight rate even where it never split.)
+std::mutex g_image_mu;
+std::vector<mrag_encoder*> g_image_handles;
+
+bool sole_image_handle(const mrag_encoder* e) {
+  std::lock_guard<std::mutex> lk(g_image_mu);
+  for (const mrag_encoder* h : g_image_handles)
+    if (h != e && h->device == e->device) return false;
+  return true;
+}
 
 // Upload n floats from host to a device buffer as f32 or f16.
 int upload(Buf& b, const float* host, int64_t n, bool to_f16, hipStream_t s) {
@@ -232,35 +263,35 @@ int layer_index(const std::string& name, const std::string& marker) {
 
 int ensure_workspace(mrag_encoder* e, int B, int T) {
   const int64_t tokens = (int64_t)B * T;
-  if (tokens <= e->ws_tokens && B <= e->ws_batch) return MRAG_OK;
+  if (tokens <= e->w->ws_tokens && B <= e->w->ws_batch) return MRAG_OK;
   if (e->last_stream) MRAG_HIP(hipEventSynchronize(e->done));  // in-flight work still reads the old buffers
   const auto& c = e->cfg;
   const int64_t D = c.hidden, I = c.intermediate;
   // per-sequence buffers grow with B, per-token ones with B * T: either can grow alone (the
   // tokenisers pad to the longest sequence of a batch, so B can grow while B * T does not)
-  if (B > e->ws_batch) {
-    if (int rc = buf_ensure(e->XG, (size_t)B * D * 4)) return rc;  // pooled rows of the last CLIP layer
-    if (int rc = buf_ensure(e->AG, (size_t)B * D * 2)) return rc;
-    if (int rc = buf_ensure(e->HG, (size_t)B * D * 2)) return rc;
-    if (int rc = buf_ensure(e->FG, (size_t)B * I * 2)) return rc;
-    if (int rc = buf_ensure(e->ROWS, (size_t)B * 4 + 256)) return rc;
-    if (int rc = buf_ensure(e->POOL16, (size_t)B * D * 2)) return rc;
+  if (B > e->w->ws_batch) {
+    if (int rc = buf_ensure(e->w->XG, (size_t)B * D * 4)) return rc;  // pooled rows of the last CLIP layer
+    if (int rc = buf_ensure(e->w->AG, (size_t)B * D * 2)) return rc;
+    if (int rc = buf_ensure(e->w->HG, (size_t)B * D * 2)) return rc;
+    if (int rc = buf_ensure(e->w->FG, (size_t)B * I * 2)) return rc;
+    if (int rc = buf_ensure(e->w->ROWS, (size_t)B * 4 + 256)) return rc;
+    if (int rc = buf_ensure(e->w->POOL16, (size_t)B * D * 2)) return rc;
     if (c.kind == MRAG_ENC_BERT_PAIR)
-      if (int rc = buf_ensure(e->POOL32, (size_t)B * D * 4)) return rc;
-    e->ws_batch = B;
+      if (int rc = buf_ensure(e->w->POOL32, (size_t)B * D * 4)) return rc;
+    e->w->ws_batch = B;
   }
-  if (tokens <= e->ws_tokens) return MRAG_OK;
-  if (int rc = buf_ensure(e->X, tokens * D * 4)) return rc;
-  if (int rc = buf_ensure(e->H16, tokens * D * 2)) return rc;
-  if (int rc = buf_ensure(e->QKV, tokens * 3 * D * 2)) return rc;
-  if (int rc = buf_ensure(e->ATT, tokens * D * 2)) return rc;
+  if (tokens <= e->w->ws_tokens) return MRAG_OK;
+  if (int rc = buf_ensure(e->w->X, tokens * D * 4)) return rc;
+  if (int rc = buf_ensure(e->w->H16, tokens * D * 2)) return rc;
+  if (int rc = buf_ensure(e->w->QKV, tokens * 3 * D * 2)) return rc;
+  if (int rc = buf_ensure(e->w->ATT, tokens * D * 2)) return rc;
   int64_t f16n = tokens * I;
   if (c.kind == MRAG_ENC_CLIP_VISION) f16n = std::max<int64_t>(f16n, tokens * 3 * c.patch_size * c.patch_size);
-  if (int rc = buf_ensure(e->F16, f16n * 2)) return rc;
+  if (int rc = buf_ensure(e->w->F16, f16n * 2)) return rc;
   if (c.kind == MRAG_ENC_CLIP_VISION) {
-    if (int rc = buf_ensure(e->PATCH, tokens * D * 4)) return rc;
+    if (int rc = buf_ensure(e->w->PATCH, tokens * D * 4)) return rc;
   }
-  e->ws_tokens = tokens;
+  e->w->ws_tokens = tokens;
   return MRAG_OK;
 }
 
@@ -301,13 +332,13 @@ int layernorm(const float* x, const int* gather, float* y32, _Float16* y16, cons
 int clip_layer(mrag_encoder* e, const Layer& L, int B, int T, const int32_t* mask, int causal, hipStream_t s) {
   const auto& c = e->cfg;
   const int D = c.hidden, I = c.intermediate, M = B * T;
-  float* X = (float*)e->X.p;
-  _Float16* H = (_Float16*)e->H16.p;
+  float* X = (float*)e->w->X.p;
+  _Float16* H = (_Float16*)e->w->H16.p;
   if (int rc = layernorm(X, nullptr, nullptr, H, L.ln1g, L.ln1b, M, D, c.ln_eps, s)) return rc;
-  if (int rc = gemm(H, L.wqkv.p, L.bqkv.p, e->QKV.p, M, 3 * D, D, 3 * D, EPI_F16, s)) return rc;
+  if (int rc = gemm(H, L.wqkv.p, L.bqkv.p, e->w->QKV.p, M, 3 * D, D, 3 * D, EPI_F16, s)) return rc;
   AttentionArgs a{};
-  a.qkv = (const _Float16*)e->QKV.p;
-  a.out = (_Float16*)e->ATT.p;
+  a.qkv = (const _Float16*)e->w->QKV.p;
+  a.out = (_Float16*)e->w->ATT.p;
   a.mask = mask;
   a.B = B;
   a.L = T;
@@ -315,11 +346,11 @@ int clip_layer(mrag_encoder* e, const Layer& L, int B, int T, const int32_t* mas
   a.causal = causal;
   a.scale = 1.0f / sqrtf((float)(D / c.heads));
   if (int rc = launch_attention(a, D / c.heads, s)) return rc;
-  if (int rc = gemm(e->ATT.p, L.wo.p, L.bo.p, X, M, D, D, D, EPI_F32_RESIDUAL, s)) return rc;
+  if (int rc = gemm(e->w->ATT.p, L.wo.p, L.bo.p, X, M, D, D, D, EPI_F32_RESIDUAL, s)) return rc;
   if (int rc = layernorm(X, nullptr, nullptr, H, L.ln2g, L.ln2b, M, D, c.ln_eps, s)) return rc;
   const int act = c.act == 0 ? EPI_F16_QUICK_GELU : EPI_F16_GELU_ERF;
-  if (int rc = gemm(H, L.w1.p, L.b1.p, e->F16.p, M, I, D, I, act, s)) return rc;
-  return gemm(e->F16.p, L.w2.p, L.b2.p, X, M, D, I, D, EPI_F32_RESIDUAL, s);
+  if (int rc = gemm(H, L.w1.p, L.b1.p, e->w->F16.p, M, I, D, I, act, s)) return rc;
+  return gemm(e->w->F16.p, L.w2.p, L.b2.p, X, M, D, I, D, EPI_F32_RESIDUAL, s);
 }
 
 // The LAST pre-LN layer of a tower that pools one row per sequence (CLIP: the class token of
@@ -334,13 +365,13 @@ int clip_layer_pooled(mrag_encoder* e, const Layer& L, int B, int T, const int32
                       hipStream_t s) {
   const auto& c = e->cfg;
   const int D = c.hidden, I = c.intermediate, M = B * T;
-  float* X = (float*)e->X.p;
-  _Float16* H = (_Float16*)e->H16.p;
+  float* X = (float*)e->w->X.p;
+  _Float16* H = (_Float16*)e->w->H16.p;
   if (int rc = layernorm(X, nullptr, nullptr, H, L.ln1g, L.ln1b, M, D, c.ln_eps, s)) return rc;
-  if (int rc = gemm(H, L.wqkv.p, L.bqkv.p, e->QKV.p, M, 3 * D, D, 3 * D, EPI_F16, s)) return rc;
+  if (int rc = gemm(H, L.wqkv.p, L.bqkv.p, e->w->QKV.p, M, 3 * D, D, 3 * D, EPI_F16, s)) return rc;
   AttentionArgs a{};
-  a.qkv = (const _Float16*)e->QKV.p;
-  a.out = (_Float16*)e->ATT.p;
+  a.qkv = (const _Float16*)e->w->QKV.p;
+  a.out = (_Float16*)e->w->ATT.p;
   a.mask = mask;
   a.B = B;
   a.L = T;
@@ -348,14 +379,14 @@ int clip_layer_pooled(mrag_encoder* e, const Layer& L, int B, int T, const int32
   a.causal = causal;
   a.scale = 1.0f / sqrtf((float)(D / c.heads));
   if (int rc = launch_attention(a, D / c.heads, s)) return rc;
-  if (int rc = launch_gather_rows(X, e->XG.p, rows, B, D * 4, s)) return rc;
-  if (int rc = launch_gather_rows(e->ATT.p, e->AG.p, rows, B, D * 2, s)) return rc;
-  float* XG = (float*)e->XG.p;
-  if (int rc = gemm(e->AG.p, L.wo.p, L.bo.p, XG, B, D, D, D, EPI_F32_RESIDUAL, s)) return rc;
-  if (int rc = layernorm(XG, nullptr, nullptr, (_Float16*)e->HG.p, L.ln2g, L.ln2b, B, D, c.ln_eps, s)) return rc;
+  if (int rc = launch_gather_rows(X, e->w->XG.p, rows, B, D * 4, s)) return rc;
+  if (int rc = launch_gather_rows(e->w->ATT.p, e->w->AG.p, rows, B, D * 2, s)) return rc;
+  float* XG = (float*)e->w->XG.p;
+  if (int rc = gemm(e->w->AG.p, L.wo.p, L.bo.p, XG, B, D, D, D, EPI_F32_RESIDUAL, s)) return rc;
+  if (int rc = layernorm(XG, nullptr, nullptr, (_Float16*)e->w->HG.p, L.ln2g, L.ln2b, B, D, c.ln_eps, s)) return rc;
   const int act = c.act == 0 ? EPI_F16_QUICK_GELU : EPI_F16_GELU_ERF;
-  if (int rc = gemm(e->HG.p, L.w1.p, L.b1.p, e->FG.p, B, I, D, I, act, s)) return rc;
-  return gemm(e->FG.p, L.w2.p, L.b2.p, XG, B, D, I, D, EPI_F32_RESIDUAL, s);
+  if (int rc = gemm(e->w->HG.p, L.w1.p, L.b1.p, e->w->FG.p, B, I, D, I, act, s)) return rc;
+  return gemm(e->w->FG.p, L.w2.p, L.b2.p, XG, B, D, I, D, EPI_F32_RESIDUAL, s);
 }
 
 // Post-LN transformer layer (BERT): X = LN(X + attn(X)); X = LN(X + ffn(X)).
@@ -363,12 +394,12 @@ int clip_layer_pooled(mrag_encoder* e, const Layer& L, int B, int T, const int32
 int bert_layer(mrag_encoder* e, const Layer& L, int B, int T, const int32_t* mask, hipStream_t s) {
   const auto& c = e->cfg;
   const int D = c.hidden, I = c.intermediate, M = B * T;
-  float* X = (float*)e->X.p;
-  _Float16* H = (_Float16*)e->H16.p;
-  if (int rc = gemm(H, L.wqkv.p, L.bqkv.p, e->QKV.p, M, 3 * D, D, 3 * D, EPI_F16, s)) return rc;
+  float* X = (float*)e->w->X.p;
+  _Float16* H = (_Float16*)e->w->H16.p;
+  if (int rc = gemm(H, L.wqkv.p, L.bqkv.p, e->w->QKV.p, M, 3 * D, D, 3 * D, EPI_F16, s)) return rc;
   AttentionArgs a{};
-  a.qkv = (const _Float16*)e->QKV.p;
-  a.out = (_Float16*)e->ATT.p;
+  a.qkv = (const _Float16*)e->w->QKV.p;
+  a.out = (_Float16*)e->w->ATT.p;
   a.mask = mask;
   a.B = B;
   a.L = T;
@@ -376,10 +407,10 @@ int bert_layer(mrag_encoder* e, const Layer& L, int B, int T, const int32_t* mas
   a.causal = 0;
   a.scale = 1.0f / sqrtf((float)(D / c.heads));
   if (int rc = launch_attention(a, D / c.heads, s)) return rc;
-  if (int rc = gemm(e->ATT.p, L.wo.p, L.bo.p, X, M, D, D, D, EPI_F32_RESIDUAL, s)) return rc;
+  if (int rc = gemm(e->w->ATT.p, L.wo.p, L.bo.p, X, M, D, D, D, EPI_F32_RESIDUAL, s)) return rc;
   if (int rc = layernorm(X, nullptr, X, H, L.ln1g, L.ln1b, M, D, c.ln_eps, s)) return rc;
-  if (int rc = gemm(H, L.w1.p, L.b1.p, e->F16.p, M, I, D, I, EPI_F16_GELU_ERF, s)) return rc;
-  if (int rc = gemm(e->F16.p, L.w2.p, L.b2.p, X, M, D, I, D, EPI_F32_RESIDUAL, s)) return rc;
+  if (int rc = gemm(H, L.w1.p, L.b1.p, e->w->F16.p, M, I, D, I, EPI_F16_GELU_ERF, s)) return rc;
+  if (int rc = gemm(e->w->F16.p, L.w2.p, L.b2.p, X, M, D, I, D, EPI_F32_RESIDUAL, s)) return rc;
   return layernorm(X, nullptr, X, H, L.ln2g, L.ln2b, M, D, c.ln_eps, s);
 }
 
@@ -427,6 +458,36 @@ int run_graph(mrag_encoder* e, uint64_t key, std::vector<const void*> sig, hipSt
   return MRAG_OK;
 }
 
+// The image tower on B images (device u8 HWC) into dst (device f32 [B][proj_dim]) on s, with
+// the workspace e->w.
+int image_forward(mrag_encoder* e, const uint8_t* img, int B, float* dst, int normalize, hipStream_t s) {
+  const auto& c = e->cfg;
+  const int S = c.image_size, P = c.patch_size, G = S / P, T = G * G + 1, D = c.hidden;
+  const int Kp = 3 * P * P;
+  float* X = (float*)e->w->X.p;
+  if (int rc = launch_vit_im2col(img, (_Float16*)e->w->F16.p, B, S, P, s)) return rc;
+  if (int rc = gemm(e->w->F16.p, e->patch_w.p, nullptr, e->w->PATCH.p, B * (T - 1), D, Kp, D, EPI_F32, s)) return rc;
+  if (int rc = launch_vit_embed_ln((const float*)e->w->PATCH.p, (const float*)e->cls.p, (const float*)e->pos.p,
+                                   (const float*)e->pre_g.p, (const float*)e->pre_b.p, X, B, T, D, c.ln_eps, s))
+    return rc;
+  if (int rc = launch_cls_rows(B, T, (int*)e->w->ROWS.p, s)) return rc;
+  const bool prune = c.layers > 0;
+  for (int i = 0; i < c.layers; ++i) {
+    if (prune && i == c.layers - 1) {
+      if (int rc = clip_layer_pooled(e, e->layers[i], B, T, nullptr, 0, (const int*)e->w->ROWS.p, s)) return rc;
+    } else if (int rc = clip_layer(e, e->layers[i], B, T, nullptr, 0, s)) {
+      return rc;
+    }
+  }
+  if (int rc = layernorm(prune ? (const float*)e->w->XG.p : X, prune ? nullptr : (const int*)e->w->ROWS.p, nullptr,
+                         (_Float16*)e->w->POOL16.p, e->post_g, e->post_b, B, D, c.ln_eps, s))
+    return rc;
+  if (int rc = gemm(e->w->POOL16.p, e->proj_w.p, nullptr, dst, B, c.proj_dim, D, c.proj_dim, EPI_F32, s)) return rc;
+  if (normalize)
+    if (int rc = mrag_l2norm_rows(dst, dst, B, c.proj_dim, s)) return rc;
+  return MRAG_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -469,12 +530,20 @@ int mrag_encoder_create(const mrag_encoder_config* cfg, int32_t device, mrag_enc
     delete e;
     return mrag::fail(MRAG_ERR_HIP, "stream: %s", hipGetErrorString(err));
   }
+  if (c.kind == MRAG_ENC_CLIP_VISION) {
+    std::lock_guard<std::mutex> lk(g_image_mu);
+    g_image_handles.push_back(e);
+  }
   *out = e;
   return MRAG_OK;
 }
 
 int mrag_encoder_destroy(mrag_encoder* e) {
   if (!e) return MRAG_OK;
+  {
+    std::lock_guard<std::mutex> lk(g_image_mu);
+    g_image_handles.erase(std::remove(g_image_handles.begin(), g_image_handles.end(), e), g_image_handles.end());
+  }
   {
     mrag::DeviceGuard g(e->device);
     (void)hipStreamSynchronize(e->stream);
@@ -487,10 +556,16 @@ int mrag_encoder_destroy(mrag_encoder* e) {
       for (Buf* b : {&L.wqkv, &L.bqkv, &L.wo, &L.bo, &L.w1, &L.b1, &L.w2, &L.b2, &L.ln1g, &L.ln1b, &L.ln2g, &L.ln2b})
         buf_free(*b);
     for (Buf* b : {&e->patch_w, &e->cls, &e->pos, &e->pre_g, &e->pre_b, &e->post_g, &e->post_b, &e->proj_w, &e->tok,
-                   &e->type0, &e->emb_g, &e->emb_b, &e->X, &e->H16, &e->QKV, &e->ATT, &e->F16, &e->PATCH, &e->IMG,
-                   &e->IDS, &e->MASK, &e->ROWS, &e->POOL16, &e->OUT, &e->pool_w, &e->pool_b, &e->cls_w, &e->cls_b,
-                   &e->POOL32, &e->TYPES, &e->XG, &e->AG, &e->HG, &e->FG})
+                   &e->type0, &e->emb_g, &e->emb_b, &e->pool_w, &e->pool_b, &e->cls_w, &e->cls_b})
       buf_free(*b);
+    for (Work& w : e->work)
+      for (Buf* b : {&w.X, &w.H16, &w.QKV, &w.ATT, &w.F16, &w.PATCH, &w.IMG, &w.IDS, &w.MASK, &w.ROWS, &w.POOL16, &w.OUT,
+                     &w.POOL32, &w.TYPES, &w.XG, &w.AG, &w.HG, &w.FG})
+        buf_free(*b);
+    for (int i = 0; i < MRAG_IMG_LANES; ++i) {
+      if (e->lane_stream[i]) (void)hipStreamDestroy(e->lane_stream[i]);
+      if (e->lane_ev[i]) (void)hipEventDestroy(e->lane_ev[i]);
+    }
     (void)hipStreamDestroy(e->stream);
   }
   delete e;
@@ -630,44 +705,68 @@ int mrag_encoder_embed_images(mrag_encoder* e, const uint8_t* images, int32_t ba
   if (int rc = begin_call(e, s, ptr_kind, stream_arg)) return rc;
   mrag::StreamDrain drain(s);  // an error return after a launch drains s (workspace reuse)
   const auto& c = e->cfg;
-  const int S = c.image_size, P = c.patch_size, G = S / P, T = G * G + 1, D = c.hidden, B = batch;
-  const int Kp = 3 * P * P;
-  if (int rc = ensure_workspace(e, B, T)) return rc;
+  const int S = c.image_size, P = c.patch_size, G = S / P, T = G * G + 1, B = batch;
+  // A lone batch of >= MRAG_IMG_LANE_MIN images runs as MRAG_IMG_LANES sub-batches ("lanes"),
+  // each on its own workspace and stream, forked from and joined back into s: one batch's GEMM
+  // rounds that leave CUs idle (the N = 768 grids: 150 tiles on 256 CUs) and its latency-bound
+  // attention / LayerNorm then overlap with the other lane's kernels, as separate calls in flight
+  // do (one batch at a time: 67.1k -> 73.5k img/s). Only the process's sole image handle on the
+  // device splits: with several handles (the drop-in's pool grows one per concurrent caller) the
+  // calls already share the GPU, and splitting them too measured 86.1k -> 75.1k img/s with three
+  // batches in flight (profiles/r5s7_lanes_ab.jsonl). Every row depends only on its image (the
+  // batch-consistency tests), so the result is bit-identical either way.
+  int lanes = (MRAG_IMG_LANES > 1 && B >= MRAG_IMG_LANE_MIN && sole_image_handle(e)) ? MRAG_IMG_LANES : 1;
+  // the lanes' streams and events are created on first use: a handle that never runs alone holds
+  // no extra stream (streams share the process's hardware queues)
+  for (int i = 0; i < lanes && lanes > 1; ++i) {
+    if (i > 0 && !e->lane_stream[i]) MRAG_HIP(hipStreamCreateWithFlags(&e->lane_stream[i], hipStreamNonBlocking));
+    if (!e->lane_ev[i]) MRAG_HIP(hipEventCreateWithFlags(&e->lane_ev[i], hipEventDisableTiming));
+  }
+  struct ResetWork {  // e->w back to work[0] on every return
+    mrag_encoder* e;
+    ~ResetWork() { e->w = &e->work[0]; }
+  } reset{e};
+  struct DrainLanes {  // an error return drains the lanes too
+    mrag_encoder* e;
+    int n;
+    bool armed = true;
+    ~DrainLanes() {
+      if (armed)
+        for (int i = 1; i < n; ++i) (void)hipStreamSynchronize(e->lane_stream[i]);
+    }
+  } drain_lanes{e, lanes};
+  e->w = &e->work[0];
   const uint8_t* img = images;
   if (ptr_kind == MRAG_PTR_HOST) {
-    if (int rc = buf_ensure(e->IMG, (size_t)B * S * S * 3)) return rc;
-    MRAG_HIP(hipMemcpyAsync(e->IMG.p, images, (size_t)B * S * S * 3, hipMemcpyHostToDevice, s));
-    img = (const uint8_t*)e->IMG.p;
+    if (int rc = buf_ensure(e->w->IMG, (size_t)B * S * S * 3)) return rc;
+    MRAG_HIP(hipMemcpyAsync(e->w->IMG.p, images, (size_t)B * S * S * 3, hipMemcpyHostToDevice, s));
+    img = (const uint8_t*)e->w->IMG.p;
   }
-  float* X = (float*)e->X.p;
-  if (int rc = launch_vit_im2col(img, (_Float16*)e->F16.p, B, S, P, s)) return rc;
-  if (int rc = gemm(e->F16.p, e->patch_w.p, nullptr, e->PATCH.p, B * (T - 1), D, Kp, D, EPI_F32, s)) return rc;
-  if (int rc = launch_vit_embed_ln((const float*)e->PATCH.p, (const float*)e->cls.p, (const float*)e->pos.p,
-                                   (const float*)e->pre_g.p, (const float*)e->pre_b.p, X, B, T, D, c.ln_eps, s))
-    return rc;
-  if (int rc = launch_cls_rows(B, T, (int*)e->ROWS.p, s)) return rc;
-  const bool prune = c.layers > 0;
-  for (int i = 0; i < c.layers; ++i) {
-    if (prune && i == c.layers - 1) {
-      if (int rc = clip_layer_pooled(e, e->layers[i], B, T, nullptr, 0, (const int*)e->ROWS.p, s)) return rc;
-    } else if (int rc = clip_layer(e, e->layers[i], B, T, nullptr, 0, s)) {
-      return rc;
-    }
-  }
-  if (int rc = layernorm(prune ? (const float*)e->XG.p : X, prune ? nullptr : (const int*)e->ROWS.p, nullptr,
-                         (_Float16*)e->POOL16.p, e->post_g, e->post_b, B, D, c.ln_eps, s))
-    return rc;
   float* dst = out;
   if (ptr_kind == MRAG_PTR_HOST) {
-    if (int rc = buf_ensure(e->OUT, (size_t)B * c.proj_dim * 4)) return rc;
-    dst = (float*)e->OUT.p;
+    if (int rc = buf_ensure(e->w->OUT, (size_t)B * c.proj_dim * 4)) return rc;
+    dst = (float*)e->w->OUT.p;
   }
-  if (int rc = gemm(e->POOL16.p, e->proj_w.p, nullptr, dst, B, c.proj_dim, D, c.proj_dim, EPI_F32, s)) return rc;
-  if (normalize)
-    if (int rc = mrag_l2norm_rows(dst, dst, B, c.proj_dim, s)) return rc;
+  if (lanes > 1) MRAG_HIP(hipEventRecord(e->lane_ev[0], s));  // fork
+  int b0 = 0;
+  for (int i = 0; i < lanes; ++i) {
+    const int nb = B / lanes + (i < B % lanes ? 1 : 0);
+    hipStream_t ls = i == 0 ? s : e->lane_stream[i];
+    if (i > 0) MRAG_HIP(hipStreamWaitEvent(ls, e->lane_ev[0], 0));
+    e->w = &e->work[i];
+    if (int rc = ensure_workspace(e, nb, T)) return rc;
+    if (int rc = image_forward(e, img + (size_t)b0 * S * S * 3, nb, dst + (size_t)b0 * c.proj_dim, normalize, ls))
+      return rc;
+    b0 += nb;
+  }
+  for (int i = 1; i < lanes; ++i) {  // join
+    MRAG_HIP(hipEventRecord(e->lane_ev[i], e->lane_stream[i]));
+    MRAG_HIP(hipStreamWaitEvent(s, e->lane_ev[i], 0));
+  }
   if (ptr_kind == MRAG_PTR_HOST)
     MRAG_HIP(hipMemcpyAsync(out, dst, (size_t)B * c.proj_dim * 4, hipMemcpyDeviceToHost, s));
   drain.armed = false;
+  drain_lanes.armed = false;
   return end_call(e, s, ptr_kind, stream_arg);
 }
 
@@ -693,41 +792,41 @@ int mrag_encoder_embed_tokens(mrag_encoder* e, const int32_t* ids, const int32_t
   const int32_t* dids = ids;
   const int32_t* dmask = mask;
   if (ptr_kind == MRAG_PTR_HOST) {
-    if (int rc = buf_ensure(e->IDS, (size_t)B * T * 4)) return rc;
-    MRAG_HIP(hipMemcpyAsync(e->IDS.p, ids, (size_t)B * T * 4, hipMemcpyHostToDevice, s));
-    dids = (const int32_t*)e->IDS.p;
+    if (int rc = buf_ensure(e->w->IDS, (size_t)B * T * 4)) return rc;
+    MRAG_HIP(hipMemcpyAsync(e->w->IDS.p, ids, (size_t)B * T * 4, hipMemcpyHostToDevice, s));
+    dids = (const int32_t*)e->w->IDS.p;
     if (mask) {
-      if (int rc = buf_ensure(e->MASK, (size_t)B * T * 4)) return rc;
-      MRAG_HIP(hipMemcpyAsync(e->MASK.p, mask, (size_t)B * T * 4, hipMemcpyHostToDevice, s));
-      dmask = (const int32_t*)e->MASK.p;
+      if (int rc = buf_ensure(e->w->MASK, (size_t)B * T * 4)) return rc;
+      MRAG_HIP(hipMemcpyAsync(e->w->MASK.p, mask, (size_t)B * T * 4, hipMemcpyHostToDevice, s));
+      dmask = (const int32_t*)e->w->MASK.p;
     }
   }
-  float* X = (float*)e->X.p;
-  _Float16* H = (_Float16*)e->H16.p;
+  float* X = (float*)e->w->X.p;
+  _Float16* H = (_Float16*)e->w->H16.p;
   const int outD = c.kind == MRAG_ENC_BERT ? D : c.proj_dim;
   float* dst = out;
   if (ptr_kind == MRAG_PTR_HOST) {
-    if (int rc = buf_ensure(e->OUT, (size_t)B * outD * 4)) return rc;
-    dst = (float*)e->OUT.p;
+    if (int rc = buf_ensure(e->w->OUT, (size_t)B * outD * 4)) return rc;
+    dst = (float*)e->w->OUT.p;
   }
   auto forward = [&](hipStream_t s) -> int {
     if (c.kind == MRAG_ENC_CLIP_TEXT) {
       if (int rc = launch_token_embed(dids, (const float*)e->tok.p, (const float*)e->pos.p, nullptr, nullptr, X, B, T,
                                       D, c.vocab, s))
         return rc;
-      if (int rc = launch_eos_rows(dids, B, T, c.eos_token_id, (int*)e->ROWS.p, s)) return rc;
+      if (int rc = launch_eos_rows(dids, B, T, c.eos_token_id, (int*)e->w->ROWS.p, s)) return rc;
       const bool prune = c.layers > 0;
       for (int i = 0; i < c.layers; ++i) {
         if (prune && i == c.layers - 1) {
-          if (int rc = clip_layer_pooled(e, e->layers[i], B, T, dmask, 1, (const int*)e->ROWS.p, s)) return rc;
+          if (int rc = clip_layer_pooled(e, e->layers[i], B, T, dmask, 1, (const int*)e->w->ROWS.p, s)) return rc;
         } else if (int rc = clip_layer(e, e->layers[i], B, T, dmask, 1, s)) {
           return rc;
         }
       }
-      if (int rc = layernorm(prune ? (const float*)e->XG.p : X, prune ? nullptr : (const int*)e->ROWS.p, nullptr,
-                             (_Float16*)e->POOL16.p, e->post_g, e->post_b, B, D, c.ln_eps, s))
+      if (int rc = layernorm(prune ? (const float*)e->w->XG.p : X, prune ? nullptr : (const int*)e->w->ROWS.p, nullptr,
+                             (_Float16*)e->w->POOL16.p, e->post_g, e->post_b, B, D, c.ln_eps, s))
         return rc;
-      if (int rc = gemm(e->POOL16.p, e->proj_w.p, nullptr, dst, B, c.proj_dim, D, c.proj_dim, EPI_F32, s)) return rc;
+      if (int rc = gemm(e->w->POOL16.p, e->proj_w.p, nullptr, dst, B, c.proj_dim, D, c.proj_dim, EPI_F32, s)) return rc;
     } else {
       if (int rc = launch_token_embed(dids, (const float*)e->tok.p, (const float*)e->pos.p, (const float*)e->type0.p,
                                       nullptr, X, B, T, D, c.vocab, s))
@@ -745,8 +844,8 @@ int mrag_encoder_embed_tokens(mrag_encoder* e, const int32_t* ids, const int32_t
   // workspace, at addresses the graph can bake in): graph replay; otherwise direct launches
   if (ptr_kind == MRAG_PTR_HOST && (int64_t)B * T <= 2048) {
     const uint64_t key = ((uint64_t)B << 32) | ((uint64_t)T << 2) | (dmask ? 2u : 0u) | (normalize ? 1u : 0u);
-    std::vector<const void*> sig = {e->X.p,  e->H16.p, e->QKV.p, e->ATT.p,    e->F16.p, e->XG.p, e->AG.p,
-                                    e->HG.p, e->FG.p,  e->ROWS.p, e->POOL16.p, e->IDS.p, e->MASK.p, e->OUT.p};
+    std::vector<const void*> sig = {e->w->X.p,  e->w->H16.p, e->w->QKV.p, e->w->ATT.p,    e->w->F16.p, e->w->XG.p, e->w->AG.p,
+                                    e->w->HG.p, e->w->FG.p,  e->w->ROWS.p, e->w->POOL16.p, e->w->IDS.p, e->w->MASK.p, e->w->OUT.p};
     if (int rc = run_graph(e, key, std::move(sig), s, forward)) return rc;
   } else if (int rc = forward(s)) {
     return rc;
@@ -779,22 +878,22 @@ int mrag_encoder_score_pairs(mrag_encoder* e, const int32_t* ids, const int32_t*
   const int32_t* dmask = mask;
   const int32_t* dtypes = type_ids;
   if (ptr_kind == MRAG_PTR_HOST) {
-    if (int rc = buf_ensure(e->IDS, (size_t)B * T * 4)) return rc;
-    MRAG_HIP(hipMemcpyAsync(e->IDS.p, ids, (size_t)B * T * 4, hipMemcpyHostToDevice, s));
-    dids = (const int32_t*)e->IDS.p;
+    if (int rc = buf_ensure(e->w->IDS, (size_t)B * T * 4)) return rc;
+    MRAG_HIP(hipMemcpyAsync(e->w->IDS.p, ids, (size_t)B * T * 4, hipMemcpyHostToDevice, s));
+    dids = (const int32_t*)e->w->IDS.p;
     if (mask) {
-      if (int rc = buf_ensure(e->MASK, (size_t)B * T * 4)) return rc;
-      MRAG_HIP(hipMemcpyAsync(e->MASK.p, mask, (size_t)B * T * 4, hipMemcpyHostToDevice, s));
-      dmask = (const int32_t*)e->MASK.p;
+      if (int rc = buf_ensure(e->w->MASK, (size_t)B * T * 4)) return rc;
+      MRAG_HIP(hipMemcpyAsync(e->w->MASK.p, mask, (size_t)B * T * 4, hipMemcpyHostToDevice, s));
+      dmask = (const int32_t*)e->w->MASK.p;
     }
     if (type_ids) {
-      if (int rc = buf_ensure(e->TYPES, (size_t)B * T * 4)) return rc;
-      MRAG_HIP(hipMemcpyAsync(e->TYPES.p, type_ids, (size_t)B * T * 4, hipMemcpyHostToDevice, s));
-      dtypes = (const int32_t*)e->TYPES.p;
+      if (int rc = buf_ensure(e->w->TYPES, (size_t)B * T * 4)) return rc;
+      MRAG_HIP(hipMemcpyAsync(e->w->TYPES.p, type_ids, (size_t)B * T * 4, hipMemcpyHostToDevice, s));
+      dtypes = (const int32_t*)e->w->TYPES.p;
     }
   }
-  float* X = (float*)e->X.p;
-  _Float16* H = (_Float16*)e->H16.p;
+  float* X = (float*)e->w->X.p;
+  _Float16* H = (_Float16*)e->w->H16.p;
   if (int rc = launch_token_embed(dids, (const float*)e->tok.p, (const float*)e->pos.p, (const float*)e->type0.p, dtypes,
                                   X, B, T, D, c.vocab, s))
     return rc;
@@ -806,7 +905,7 @@ int mrag_encoder_score_pairs(mrag_encoder* e, const int32_t* ids, const int32_t*
   pg.A = H;
   pg.W = (const _Float16*)e->pool_w.p;
   pg.bias = (const float*)e->pool_b.p;
-  pg.C = e->POOL32.p;
+  pg.C = e->w->POOL32.p;
   pg.M = B;
   pg.N = D;
   pg.K = D;
@@ -816,10 +915,10 @@ int mrag_encoder_score_pairs(mrag_encoder* e, const int32_t* ids, const int32_t*
   if (int rc = launch_gemm(pg, EPI_F32, s)) return rc;
   float* dst = out;
   if (ptr_kind == MRAG_PTR_HOST) {
-    if (int rc = buf_ensure(e->OUT, (size_t)B * NL * 4)) return rc;
-    dst = (float*)e->OUT.p;
+    if (int rc = buf_ensure(e->w->OUT, (size_t)B * NL * 4)) return rc;
+    dst = (float*)e->w->OUT.p;
   }
-  if (int rc = launch_cls_head((const float*)e->POOL32.p, (const float*)e->cls_w.p, (const float*)e->cls_b.p, dst, B, D,
+  if (int rc = launch_cls_head((const float*)e->w->POOL32.p, (const float*)e->cls_w.p, (const float*)e->cls_b.p, dst, B, D,
                                NL, s))
     return rc;
   if (ptr_kind == MRAG_PTR_HOST) MRAG_HIP(hipMemcpyAsync(out, dst, (size_t)B * NL * 4, hipMemcpyDeviceToHost, s));
