@@ -666,9 +666,9 @@ def fusion_leg(world: int, rank: int, local: int, steps: int, warmup: int):
     # batches runs them. At N > 1 everything stays in one thread: the collectives share one
     # communicator and must be issued in the same order on every rank. MRAG_FUSION_STREAMS=1
     # serialises the branches, MRAG_FUSION_INFLIGHT sets the steps in flight (A/B timing; four
-    # measured +4.1 / +1.3 / +2.8 % over two in three interleaved pairs on one box,
-    # profiles/r4s24_fusion_inflight_ab.txt — within the box-to-box spread; re-checked in round 5,
-    # profiles/r5_fusion_inflight_ab.txt).
+    # measured +4.1 / +1.3 / +2.8 % over two in three interleaved pairs on one box in round 4,
+    # profiles/r4s24_fusion_inflight_ab.txt, and -3.9 / +2.0 / +0.7 % in round 5,
+    # profiles/r5_fusion_inflight_ab.txt: no difference beyond the noise; four kept).
     two = world == 1 and os.environ.get("MRAG_FUSION_STREAMS", "2") != "1"
     slots = max(1, int(os.environ.get("MRAG_FUSION_INFLIGHT", "4"))) if two else 1
     from concurrent.futures import ThreadPoolExecutor
