@@ -80,12 +80,45 @@ def _prepare_metadata(chunk: Chunk) -> Dict[str, Any]:
     return meta
 
 
+_QUERY_POOL = None  # one worker thread: the CLIP-text query encode beside the MiniLM one
+_SIDE_STREAMS: Dict[int, Any] = {}
+
+
+def _image_query_on_side_stream(query: str, dev: int) -> np.ndarray:
+    import torch
+
+    s = _SIDE_STREAMS.get(dev)
+    if s is None:
+        s = _SIDE_STREAMS.setdefault(dev, torch.cuda.Stream(device=dev))
+    with torch.cuda.device(dev), torch.cuda.stream(s):
+        return embed_query_for_images(query)
+
+
 def _get_embeddings(query: str) -> Tuple[np.ndarray, np.ndarray]:
+    """Both query vectors (reference :120-129: MiniLM, then CLIP text). On a GPU the two B = 1
+    encodes are independent chains of small kernels, so the CLIP-text one runs in a worker thread
+    on its own HIP stream while this thread runs MiniLM (the pair takes ~the longer of the two
+    instead of their sum; the vectors are the same, and an exception from either propagates)."""
+    global _QUERY_POOL
     cached = get_query_embeddings(query)
     if cached:
         return cached
-    text_vec = embed_text_batch([query])
-    image_vec = embed_query_for_images(query)
+    import torch
+
+    fut = None
+    if torch.cuda.is_available():
+        if _QUERY_POOL is None:
+            from concurrent.futures import ThreadPoolExecutor
+
+            _QUERY_POOL = ThreadPoolExecutor(max_workers=1, thread_name_prefix="mrag-query")
+        fut = _QUERY_POOL.submit(_image_query_on_side_stream, query, torch.cuda.current_device())
+    try:
+        text_vec = embed_text_batch([query])
+    except BaseException:
+        if fut is not None:
+            fut.exception()  # let the image branch finish; the text error is the one raised
+        raise
+    image_vec = fut.result() if fut is not None else embed_query_for_images(query)
     set_query_embeddings(query, text_vec[0] if text_vec.size else np.zeros(384, dtype=np.float32), image_vec)
     if text_vec.size == 0:
         text_vec = np.zeros((1, 384), dtype=np.float32)
