@@ -221,6 +221,20 @@ int mrag_encoder_score_pairs(mrag_encoder* enc, const int32_t* ids, const int32_
 int mrag_image_resize_crop(const uint8_t* pixels, const int64_t* offsets, const int32_t* widths,
                            const int32_t* heights, int32_t n, int32_t size, uint8_t* out, void* stream);
 
+/* K13: baseline JPEG decode on the GPU, byte-identical to Pillow's decode + convert("RGB")
+ * (replaces the per-file Image.open(path).convert("RGB") of the reference's embed_images_batch,
+ * app/ml/embeddings.py:82-89, for the JPEGs it supports).
+ * mrag_jpeg_probe: host-only header parse of one file; returns 1 and the size when K13 decodes it
+ * (baseline / extended sequential Huffman, 8-bit, 1 or 3 components, 4:4:4 / 4:2:2 / 4:2:0,
+ * restart intervals), 0 when the caller must decode it on the host (progressive, arithmetic,
+ * CMYK, RGB-coded, other sampling, tiny chroma), negative on bad arguments. */
+int mrag_jpeg_probe(const uint8_t* data, int64_t size, int32_t* width, int32_t* height);
+/* mrag_jpeg_decode: n files (host bytes, every one probed 1) decoded into device memory `out`,
+ * file i as H x W x 3 u8 RGB at byte offset out_offsets[i] (host array) — the pixel layout
+ * mrag_image_resize_crop takes. Synchronous on `stream`. */
+int mrag_jpeg_decode(const uint8_t* const* files, const int64_t* sizes, int32_t n, uint8_t* out,
+                     const int64_t* out_offsets, int32_t device, void* stream);
+
 /* K3 building block: C[M][N] (op)= A[M][K] . W[N][K]^T + bias (device pointers;
  * A, W fp16 row-major; epilogue 0 f16 out, 1 f16 quick_gelu, 2 f16 gelu_erf,
  * 3 f32 C += , 4 f32 out). N % 128 == 0, K % 64 == 0; bias and C 16-byte aligned. */

@@ -45,6 +45,8 @@ SIGNATURES = {
     "mrag_fuse_scores": (_c_int, [_vp, _c_int, _vp, _c_int, _c_i64, _c_int, _vp, _vp, _vp]),
     "mrag_image_resize_crop": (_c_int, [_vp, ctypes.POINTER(_c_i64), ctypes.POINTER(_c_int),
                                         ctypes.POINTER(_c_int), _c_int, _c_int, _vp, _vp]),
+    "mrag_jpeg_probe": (_c_int, [ctypes.c_char_p, _c_i64, ctypes.POINTER(_c_int), ctypes.POINTER(_c_int)]),
+    "mrag_jpeg_decode": (_c_int, [_vp, _vp, _c_int, _vp, _vp, _c_int, _vp]),
 }
 
 _lib: Optional[ctypes.CDLL] = None

@@ -19,7 +19,8 @@ from typing import Optional, Sequence, Tuple
 import numpy as np
 
 from app.encoders import CLIP_TEXT_B32, CLIP_VISION_B32, MINILM_L6, GpuEncoder, load_encoder
-from app.encoders.preprocess import decode_batch, load_batch, load_batch_device, resize_crop_device
+from app.encoders.preprocess import (load_batch, load_batch_device, prepare_batch, resize_images, upload_decode,
+                                      upload_resize)
 from app.encoders.tokenize import ClipTokenizer, WordPieceTokenizer
 from app.encoders.weights import encoder_weights, resolve_model_dir, synth_state_dict, synthetic_allowed, SYNTHETIC_ENV
 
@@ -272,15 +273,25 @@ class ClipProcessor:
             return BatchInputs(input_ids=ids, attention_mask=mask)
         raise ValueError("ClipProcessor needs images= or text=")
 
-    # The two halves of images= for a caller that pipelines batches (embed_images_batch decodes
-    # batch i + 1 on the host while batch i is resized and encoded on the GPU).
+    # The two halves of images= for a caller that pipelines batches (embed_images_batch prepares
+    # batch i + 1 on the host — file reads, Pillow decode of what K13 does not take — while batch i
+    # is decoded, resized and encoded on the GPU).
     @staticmethod
     def decode(images):
-        return decode_batch(list(images))
+        return prepare_batch(list(images))
 
     @staticmethod
-    def from_decoded(arrays):
-        return BatchInputs(images_u8=resize_crop_device(arrays, device=_device_index()))
+    def from_decoded(prepared):
+        return BatchInputs(images_u8=upload_resize(prepared, device=_device_index()))
+
+    # A group of several encoder batches: one K13 launch for the group, then K0 per batch.
+    @staticmethod
+    def decode_device(prepared):
+        return upload_decode(prepared, device=_device_index())
+
+    @staticmethod
+    def from_device(imgs, start, count):
+        return BatchInputs(images_u8=resize_images(imgs, start, count, device=_device_index()))
 
 
 class CrossEncoderModel:

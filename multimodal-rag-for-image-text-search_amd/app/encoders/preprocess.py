@@ -3,9 +3,11 @@ crop 224 -> u8 HWC. Everything after (rescale, mean/std normalise, layout) is fu
 the GPU patch-embed kernel.
 
 Two implementations with identical bytes: ``load_batch_device`` (the default for the
-native encoders) decodes on host threads and runs the resize + crop on the GPU
-(``mrag_image_resize_crop``, K0 in csrc/imgprep.hip — Pillow's fixed-point resampler
-restated); ``load_batch`` does all of it with PIL on the host.
+native encoders) decodes baseline JPEGs on the GPU (``mrag_jpeg_decode``, K13 in csrc/jpeg.hip —
+libjpeg-turbo's decode as Pillow runs it, restated), every other file on host threads with
+Pillow, and runs the resize + crop on the GPU (``mrag_image_resize_crop``, K0 in
+csrc/imgprep.hip — Pillow's fixed-point resampler restated); ``load_batch`` does all of it with
+PIL on the host. ``MRAG_HOST_DECODE=1`` decodes every file on the host (A/B timing).
 
 Restates CLIPImageProcessor's PIL path (the processor the reference loads for
 openai/clip-vit-base-patch32, app/ml/embeddings.py:39-43, 84-85):
@@ -16,6 +18,8 @@ Checked against transformers' CLIPImageProcessor in tests/test_compat_cpu.py.
 """
 from __future__ import annotations
 
+import ctypes
+import io
 import os
 import threading
 from concurrent.futures import ThreadPoolExecutor
@@ -148,10 +152,115 @@ def decode_batch(items: Sequence[Union[str, Path, Image.Image]]) -> List[np.ndar
     return list(_pool().map(decode_rgb, items))
 
 
-def load_batch_device(items: Sequence[Union[str, Path, Image.Image]], device: int = 0):
-    """Decode on the host thread pool, resize + crop on the GPU: u8 [n, 224, 224, 3] CUDA tensor."""
-    if len(items) == 0:
-        import torch
+def _prepare_one(x):
+    """A file K13 decodes on the GPU -> (bytes, (h, w)), None; anything else (a PIL image, a PNG,
+    a progressive JPEG ...) -> None, its u8 HxWx3 RGB decoded here with Pillow."""
+    if isinstance(x, Image.Image):
+        return None, decode_rgb(x)
+    with open(x, "rb") as f:
+        b = f.read()
+    if b[:2] == b"\xff\xd8" and os.environ.get("MRAG_HOST_DECODE") != "1":
+        from app import _native
 
-        return torch.empty((0, SIZE, SIZE, 3), dtype=torch.uint8, device=torch.device("cuda", device))
-    return resize_crop_device(decode_batch(items), device=device)
+        w, h = ctypes.c_int32(0), ctypes.c_int32(0)
+        if _native.load().mrag_jpeg_probe(b, len(b), ctypes.byref(w), ctypes.byref(h)) == 1:
+            return (b, (h.value, w.value)), None
+    with Image.open(io.BytesIO(b)) as im:
+        return None, np.asarray(im.convert("RGB"), dtype=np.uint8)
+
+
+def prepare_batch(items: Sequence[Union[str, Path, Image.Image]]) -> list:
+    """The host half of ``load_batch_device`` on the process-wide pool: file bytes of the JPEGs the
+    GPU decodes, Pillow arrays of everything else (embed_images_batch runs it for the next batch
+    while the GPU works on the current one)."""
+    return list(_pool().map(_prepare_one, items)) if len(items) else []
+
+
+class DeviceImages:
+    """Decoded RGB images of a group in one device buffer: image i is dims[i] = (h, w) at byte
+    offsets[i] of ``pix`` (u8 HxWx3) — what K0 resizes from."""
+
+    def __init__(self, pix, offsets: np.ndarray, dims: np.ndarray):
+        self.pix, self.offsets, self.dims = pix, offsets, dims
+
+    def __len__(self):
+        return len(self.offsets)
+
+
+def upload_decode(prepared: list, device: int = 0) -> DeviceImages:
+    """The device half's decode: K13 decodes the group's JPEGs straight into one pixel buffer and
+    the host-decoded images are copied in after them (one pinned copy). K13 decodes every file
+    of a launch in parallel (one wave per entropy-coded segment) at the pace of the largest, so a
+    larger group costs about the same time: embed_images_batch decodes several encoder batches
+    per launch."""
+    import torch
+
+    from app import _native
+
+    n = len(prepared)
+    dev = torch.device("cuda", device)
+    for j, a in prepared:
+        if a is not None and (a.ndim != 3 or a.shape[2] != 3):
+            raise ValueError(f"expected HxWx3 u8 images, got shape {a.shape}")
+    dims = np.array([j[1] if j is not None else a.shape[:2] for j, a in prepared], dtype=np.int64).reshape(n, 2)
+    sizes = dims[:, 0] * dims[:, 1] * 3
+    host = [i for i in range(n) if prepared[i][1] is not None]
+    jpeg = [i for i in range(n) if prepared[i][0] is not None]
+    offsets = np.zeros(n, dtype=np.int64)  # host-decoded images first (one contiguous copy), then K13's
+    pos = 0
+    for i in host + jpeg:
+        offsets[i] = pos
+        pos += int(sizes[i])
+    pix = torch.empty(max(pos, 1), dtype=torch.uint8, device=dev)
+    with torch.cuda.device(dev):
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        if host:
+            nh = int(sum(int(sizes[i]) for i in host))
+            staging = torch.empty(nh, dtype=torch.uint8, pin_memory=True)
+            sv = staging.numpy()
+            for i in host:
+                sv[offsets[i]:offsets[i] + sizes[i]] = np.ascontiguousarray(prepared[i][1], dtype=np.uint8).reshape(-1)
+            pix[:nh].copy_(staging, non_blocking=True)
+        if jpeg:
+            files = (ctypes.c_char_p * len(jpeg))(*[prepared[i][0][0] for i in jpeg])
+            fsz = np.array([len(prepared[i][0][0]) for i in jpeg], dtype=np.int64)
+            offs = np.ascontiguousarray(offsets[jpeg])
+            _native.call("mrag_jpeg_decode", ctypes.cast(files, ctypes.c_void_p), fsz.ctypes.data, len(jpeg),
+                         pix.data_ptr(), offs.ctypes.data, device, stream)
+    return DeviceImages(pix, offsets, dims)
+
+
+def resize_images(imgs: DeviceImages, start: int = 0, count: int = -1, device: int = 0, size: int = SIZE):
+    """K0 resize + centre crop of images [start, start + count) of a decoded group -> u8
+    [count, size, size, 3] CUDA tensor."""
+    import torch
+
+    from app import _native
+
+    stop = len(imgs) if count < 0 else min(len(imgs), start + count)
+    n = max(0, stop - start)
+    dev = torch.device("cuda", device)
+    out = torch.empty((n, size, size, 3), dtype=torch.uint8, device=dev)
+    if n == 0:
+        return out
+    offsets = np.ascontiguousarray(imgs.offsets[start:stop], dtype=np.int64)
+    widths = np.ascontiguousarray(imgs.dims[start:stop, 1], dtype=np.int32)
+    heights = np.ascontiguousarray(imgs.dims[start:stop, 0], dtype=np.int32)
+    with torch.cuda.device(dev):
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        _native.call("mrag_image_resize_crop", imgs.pix.data_ptr(),
+                     offsets.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+                     widths.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                     heights.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), n, size, out.data_ptr(), stream)
+    return out
+
+
+def upload_resize(prepared: list, device: int = 0, size: int = SIZE):
+    """The whole device half: decode (K13 + host copies), then K0 -> u8 [n, size, size, 3]."""
+    return resize_images(upload_decode(prepared, device=device), device=device, size=size)
+
+
+def load_batch_device(items: Sequence[Union[str, Path, Image.Image]], device: int = 0):
+    """Decode (baseline JPEG on the GPU, the rest on the host thread pool), resize + crop on the
+    GPU: u8 [n, 224, 224, 3] CUDA tensor."""
+    return upload_resize(prepare_batch(items), device=device)

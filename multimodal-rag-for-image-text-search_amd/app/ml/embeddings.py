@@ -24,6 +24,7 @@ import numpy as np
 from app.settings import settings
 
 _TEXT_MODEL: Optional[Any] = None
+_DECODE_GROUP_BATCHES = 4  # encoder batches per K13 decode launch in embed_images_batch
 _CLIP_MODEL: Optional[Any] = None
 _CLIP_PROCESSOR: Optional[Any] = None
 
@@ -108,18 +109,23 @@ def embed_images_batch(paths: Sequence[Path], batch_size: int = 8) -> np.ndarray
     paths = list(paths)
     out: List[np.ndarray] = []
     if native and os.environ.get("MRAG_HOST_RESIZE") != "1":
-        # decode-bound ingest: the host decodes batch i + 1 while the GPU resizes and encodes batch i
+        # decode-bound ingest: the host prepares group g + 1 (file reads, Pillow for what K13 does
+        # not take) while the GPU decodes group g's JPEGs in one K13 launch (its time is set by the
+        # largest file, not by the count) and resizes + encodes it batch by batch
         from concurrent.futures import ThreadPoolExecutor
 
-        starts = list(range(0, len(paths), step))
+        group = _DECODE_GROUP_BATCHES * step
+        starts = list(range(0, len(paths), group))
         with ThreadPoolExecutor(max_workers=1) as ahead:
-            nxt = ahead.submit(processor.decode, paths[0:step])
+            nxt = ahead.submit(processor.decode, paths[0:group])
             for i, start in enumerate(starts):
-                arrays = nxt.result()
+                prepared = nxt.result()
                 if i + 1 < len(starts):
-                    nxt = ahead.submit(processor.decode, paths[starts[i + 1]:starts[i + 1] + step])
-                inputs = processor.from_decoded(arrays)
-                out.append(_to_numpy(model.get_image_features(**_kwargs(inputs))))
+                    nxt = ahead.submit(processor.decode, paths[starts[i + 1]:starts[i + 1] + group])
+                imgs = processor.decode_device(prepared)
+                for c0 in range(0, len(prepared), step):
+                    inputs = processor.from_device(imgs, c0, step)
+                    out.append(_to_numpy(model.get_image_features(**_kwargs(inputs))))
         return _normalize(np.vstack(out))
     for start in range(0, len(paths), step):
         batch_paths = paths[start:start + step]

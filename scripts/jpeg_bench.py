@@ -1,0 +1,77 @@
+#!/usr/bin/env python3
+"""K13 vs Pillow on the bench's synthetic JPEG files (bench._write_images: 640x480 .. 1024x768,
+q90, 4:2:0): decode img/s of Pillow on the decode pool and of mrag_jpeg_decode (batches of 256,
+bytes already in host memory), and load_batch_device end to end (read + probe + decode + K0)."""
+import ctypes
+import json
+import os
+import shutil
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "multimodal-rag-for-image-text-search_amd"), ROOT]
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+from app import _native  # noqa: E402
+from app.encoders.preprocess import decode_batch, decode_workers, load_batch_device  # noqa: E402
+
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
+d = tempfile.mkdtemp(prefix="mrag_jpeg_bench_")
+try:
+    paths = [p for p in bench._write_images(d, n + n // 3) if p.endswith(".jpg")][:n]
+    raw = [open(p, "rb").read() for p in paths]
+    dev = torch.device("cuda", 0)
+    res = {"files": len(paths), "mb": round(sum(map(len, raw)) / 1e6, 1), "decode_threads": decode_workers()}
+    decode_batch(paths[:64])
+    t0 = time.perf_counter()
+    arrays = decode_batch(paths)
+    res["pillow_pool_img_s"] = round(len(paths) / (time.perf_counter() - t0), 1)
+    offs_all = []
+    for i in range(0, len(paths), 256):
+        sz = np.array([a.size for a in arrays[i:i + 256]], dtype=np.int64)
+        o = np.zeros(len(sz), dtype=np.int64)
+        o[1:] = np.cumsum(sz)[:-1]
+        offs_all.append((o, int(sz.sum())))
+    stream = torch.cuda.current_stream(dev).cuda_stream
+
+    def k13():
+        outs = []
+        for bi, i in enumerate(range(0, len(paths), 256)):
+            chunk = raw[i:i + 256]
+            o, tot = offs_all[bi]
+            out = torch.empty(tot, dtype=torch.uint8, device=dev)
+            files = (ctypes.c_char_p * len(chunk))(*chunk)
+            fsz = np.array([len(b) for b in chunk], dtype=np.int64)
+            _native.call("mrag_jpeg_decode", ctypes.cast(files, ctypes.c_void_p), fsz.ctypes.data, len(chunk),
+                         out.data_ptr(), o.ctypes.data, 0, stream)
+            outs.append(out)
+        return outs
+
+    k13()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    outs = k13()
+    torch.cuda.synchronize()
+    res["k13_img_s"] = round(len(paths) / (time.perf_counter() - t0), 1)
+    ok = True
+    for bi, i in enumerate(range(0, len(paths), 256)):
+        h = outs[bi].cpu().numpy()
+        o, _ = offs_all[bi]
+        for j, a in enumerate(arrays[i:i + 256]):
+            ok &= bool(np.array_equal(h[o[j]:o[j] + a.size].reshape(a.shape), a))
+    res["k13_equals_pillow"] = ok
+    load_batch_device(paths[:256])
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(0, len(paths), 256):
+        load_batch_device(paths[i:i + 256])
+    torch.cuda.synchronize()
+    res["load_batch_device_img_s"] = round(len(paths) / (time.perf_counter() - t0), 1)
+    print(json.dumps(res), flush=True)
+finally:
+    shutil.rmtree(d, ignore_errors=True)

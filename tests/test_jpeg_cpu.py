@@ -1,0 +1,67 @@
+"""K13's decode arithmetic (csrc/jpeg_core.h + jpeg_parse.h: the functions the device kernels
+call) run on the CPU and compared with Pillow (the reference's decoder) byte for byte; the
+library's host-side probe classifies supported / unsupported files. No GPU."""
+from __future__ import annotations
+
+import ctypes
+import os
+import shutil
+import subprocess
+
+import numpy as np
+import pytest
+
+from _jpeg_cases import pillow_rgb, supported_cases, unsupported_cases
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "multimodal-rag-for-image-text-search_amd", "csrc")
+
+
+@pytest.fixture(scope="module")
+def host_check(tmp_path_factory):
+    hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    if not os.path.exists(hipcc):
+        pytest.skip("hipcc not available")
+    so = str(tmp_path_factory.mktemp("jpeg") / "jpeg_host_check.so")
+    subprocess.run([hipcc, "-O2", "-fPIC", "-shared", f"-I{CSRC}", os.path.join(ROOT, "scripts", "jpeg_host_check.hip"),
+                    "-o", so], check=True, capture_output=True, timeout=300)
+    lib = ctypes.CDLL(so)
+    lib.jpeg_host_decode.argtypes = [ctypes.c_char_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]
+    return lib
+
+
+def _decode(lib, b: bytes):
+    wh = np.zeros(2, np.int32)
+    cap = 64 << 20
+    out = np.zeros(cap, np.uint8)
+    r = lib.jpeg_host_decode(b, len(b), out.ctypes.data, cap, wh.ctypes.data)
+    if r != 1:
+        return None
+    w, h = int(wh[0]), int(wh[1])
+    return out[:w * h * 3].reshape(h, w, 3)
+
+
+def test_core_matches_pillow(host_check):
+    for name, b in supported_cases():
+        got = _decode(host_check, b)
+        assert got is not None, name
+        np.testing.assert_array_equal(got, pillow_rgb(b), err_msg=name)
+
+
+def test_core_refuses_unsupported(host_check):
+    for name, b in unsupported_cases():
+        assert _decode(host_check, b) is None, name
+
+
+def test_library_probe():
+    from app import _native
+
+    lib = _native.load()
+    w, h = ctypes.c_int32(0), ctypes.c_int32(0)
+    for name, b in supported_cases()[:12]:
+        assert lib.mrag_jpeg_probe(b, len(b), ctypes.byref(w), ctypes.byref(h)) == 1, name
+        assert (h.value, w.value) == pillow_rgb(b).shape[:2], name
+    for name, b in unsupported_cases():
+        assert lib.mrag_jpeg_probe(b, len(b), ctypes.byref(w), ctypes.byref(h)) == 0, name
+    png = b"\x89PNG\r\n\x1a\n" + b"\0" * 32
+    assert lib.mrag_jpeg_probe(png, len(png), ctypes.byref(w), ctypes.byref(h)) == 0
