@@ -2,13 +2,16 @@
 // device). Reference: app/ml/embeddings.py:82-89 decodes every file with Pillow
 // (Image.open(path).convert("RGB")); the arithmetic restated in jpeg_core.h gives Pillow's bytes.
 //
-// A batch of files is parsed on the host (jpeg_parse.h: tables, geometry, entropy-coded segments),
-// the entropy-coded bytes of all files go to the device in one copy, and three kernels run:
-//   K13a jpeg_huff_kernel   one single-lane workgroup per entropy-coded segment (a whole image, or
-//                           one restart interval): Huffman decode into zeroed int16 coefficient
-//                           blocks. A one-thread workgroup makes every value wave-uniform, so the
-//                           decoder runs on the scalar unit with its tables read through the
-//                           scalar cache; segments run in parallel across CUs.
+// A batch of files is parsed on the host (jpeg_parse.h: tables, geometry, entropy-coded segments;
+// host threads, one file each), every segment's bytes are unstuffed into one pinned buffer and go
+// to the device in one copy, and three kernels run:
+//   K13a jpeg_huff_par_kernel  one workgroup per entropy-coded segment (a whole image, or one
+//                           restart interval), one chunk of the segment's bits per lane (up to
+//                           256): self-synchronising parallel Huffman decode (jpeg_core.h,
+//                           par_run) into zeroed int16 coefficient blocks, the same tokens and
+//                           values as the sequential decoder (round 5 first shipped that one, one
+//                           single-lane workgroup per segment: 70-78 ms per launch, the largest
+//                           file's serial chain).
 //   K13b jpeg_idct_kernel   one thread per 8x8 block: dequantise + islow IDCT into the planes.
 //   K13c jpeg_color_kernel  one thread per output pixel: fancy chroma upsampling + YCbCr -> RGB,
 //                           H x W x 3 u8 at the caller's offset (the layout K0 resizes from).
@@ -17,6 +20,7 @@
 #include <algorithm>
 #include <cstring>
 #include <mutex>
+#include <thread>
 #include <vector>
 
 #include "common.h"
@@ -26,11 +30,98 @@ using namespace mrag_jpeg;
 
 namespace {
 
-__global__ __launch_bounds__(1) void jpeg_huff_kernel(const Image* __restrict__ imgs, const Segment* __restrict__ segs,
-                                                      const uint8_t* __restrict__ ecs, int16_t* __restrict__ coef) {
-  const Segment sg = segs[blockIdx.x];
-  const Image& im = imgs[sg.img];
-  decode_segment(im, ecs + sg.off, sg.len, sg.mcu0, sg.mcus, coef + im.coef_off * 64);
+// one entropy-coded segment on the device: unstuffed bytes at uoff (16-byte aligned, zero to the
+// next 16-byte boundary), nbits = 8 x their count
+struct ParSeg {
+  int64_t uoff;
+  uint32_t nbits;
+  int32_t img, mcu0, mcus;
+};
+
+// K13a: the passes of decode_segment_par (jpeg_parse.h, its host emulation), one lane per chunk.
+__global__ __launch_bounds__(PAR_LANES) void jpeg_huff_par_kernel(const Image* __restrict__ imgs,
+                                                                  const ParSeg* __restrict__ segs,
+                                                                  const uint8_t* __restrict__ ecs,
+                                                                  int16_t* __restrict__ coef) {
+  __shared__ PTabs T;
+  __shared__ PState ex[PAR_LANES];
+  __shared__ PCheck cps[PAR_NCP * PAR_LANES];
+  __shared__ int32_t scan[4][PAR_LANES];
+  const ParSeg sg = segs[blockIdx.x];
+  const Image* im = imgs + sg.img;
+  const int t = threadIdx.x;
+  {
+    constexpr int W = (int)(4 * sizeof(Huff) / 4);
+    const uint32_t* src = (const uint32_t*)&im->dc[0];
+    uint32_t* dst = (uint32_t*)&T.h[0];
+    for (int i = t; i < W; i += PAR_LANES) dst[i] = src[i];
+    if (t == 0) make_ptab_ids(*im, T);
+  }
+  __syncthreads();
+  int nl;
+  uint32_t chunk;
+  par_geom(sg.nbits, nl, chunk);
+  const bool act = t < nl;
+  uint32_t start = 0, end = 0, cpos[PAR_NCP];
+  par_lane(sg.nbits, nl, chunk, act ? t : 0, start, end, cpos);
+  const uint8_t* data = ecs + sg.uoff;
+  const uint32_t nbytes = sg.nbits / 8;
+  PBits br;
+  PState entry{start, 0}, myexit{start, 0};
+  int32_t tot[4] = {0, 0, 0, 0};
+  if (act) {
+    br.init(data, nbytes, start);
+    PState st = entry;
+    par_run<PAR_RECORD>(T, br, st, end, tot, cps + t, PAR_LANES, cpos, nullptr, im, nullptr, 0, 0, 0, nullptr);
+    myexit = st;
+    ex[t] = st;
+  }
+  while (true) {  // resynchronisation rounds, until no exit changes
+    __syncthreads();
+    bool redo = false;
+    PState e{0, 0};
+    if (act && t > 0) {
+      e = ex[t - 1];
+      redo = e.p != entry.p || e.bk != entry.bk;
+    }
+    __syncthreads();  // every exit read before any is rewritten
+    int changed = 0;
+    if (redo) {
+      entry = e;
+      PState st = e;
+      br.init(data, nbytes, e.p);
+      int32_t m[4] = {0, 0, 0, 0};
+      const bool synced =
+          par_run<PAR_SYNC>(T, br, st, end, m, cps + t, PAR_LANES, cpos, tot, im, nullptr, 0, 0, 0, nullptr);
+      for (int q = 0; q < 4; ++q) tot[q] = m[q];
+      if (!synced && (st.p != myexit.p || st.bk != myexit.bk)) {
+        myexit = st;
+        ex[t] = st;
+        changed = 1;
+      }
+    }
+    if (!__syncthreads_or(changed)) break;
+  }
+  // first block and DC predictors of every lane: exclusive prefix sums of the chunk totals
+  for (int q = 0; q < 4; ++q) scan[q][t] = act ? tot[q] : 0;
+  __syncthreads();
+  for (int off = 1; off < PAR_LANES; off <<= 1) {
+    int32_t v[4];
+    for (int q = 0; q < 4; ++q) v[q] = t >= off ? scan[q][t - off] : 0;
+    __syncthreads();
+    for (int q = 0; q < 4; ++q) scan[q][t] += v[q];
+    __syncthreads();
+  }
+  if (act) {
+    int32_t pre[4];
+    for (int q = 0; q < 4; ++q) pre[q] = scan[q][t] - tot[q];
+    int32_t pred[3] = {pre[1], pre[2], pre[3]};
+    PState st = entry;  // exact: lane 0 starts at bit 0, lane t at lane t - 1's final exit
+    br.init(data, nbytes, st.p);
+    int32_t n[4] = {0, 0, 0, 0};
+    par_run<PAR_WRITE>(T, br, st, t == nl - 1 ? 0xFFFFFFFFu : end, n, nullptr, 0, nullptr, nullptr, im,
+                       coef + im->coef_off * 64, pre[0], (int64_t)sg.mcus * T.bpm, sg.mcu0, pred);
+  }
 }
 
 __global__ __launch_bounds__(256) void jpeg_idct_kernel(const Image* __restrict__ imgs, const int16_t* __restrict__ coef,
@@ -107,39 +198,55 @@ int mrag_jpeg_decode(const uint8_t* const* files, const int64_t* sizes, int32_t 
   if (n == 0) return MRAG_OK;
   MRAG_REQUIRE(files && sizes && out && out_offsets, "NULL argument");
   MRAG_REQUIRE(device >= 0 && device < 64, "bad device %d", device);
+  for (int i = 0; i < n; ++i) MRAG_REQUIRE(files[i] != nullptr && sizes[i] >= 0, "bad file %d", i);
   mrag::DeviceGuard g(device);
   Ctx& C = g_ctx[device];
   std::lock_guard<std::mutex> lk(C.mu);
   hipStream_t s = (hipStream_t)stream;
 
+  // host threads over the files: parse, then (below) unstuff into the pinned stage
+  const int nth = (int)std::max<int64_t>(1, std::min<int64_t>({8, (int64_t)std::thread::hardware_concurrency(), (n + 15) / 16}));
+  auto parallel = [&](auto fn) {
+    std::vector<std::thread> th;
+    for (int w = 1; w < nth; ++w) th.emplace_back([&, w] { for (int i = w; i < n; i += nth) fn(i); });
+    for (int i = 0; i < n; i += nth) fn(i);
+    for (auto& x : th) x.join();
+  };
+  std::vector<Parsed> P((size_t)n);
+  std::vector<char> ok((size_t)n, 0);
+  parallel([&](int i) { ok[i] = parse(files[i], sizes[i], P[i]) ? 1 : 0; });
   std::vector<Image> imgs((size_t)n);
-  std::vector<Segment> segs;
-  std::vector<int64_t> ecs_at((size_t)n);
-  int64_t ecs_total = 0, blocks = 0, planes = 0, max_blocks = 0, max_pix = 0;
+  std::vector<ParSeg> segs;
+  std::vector<int64_t> seg_src;  // raw segment start in its file
+  std::vector<int64_t> seg_len;
+  int64_t stage_bytes = 0, blocks = 0, planes = 0, max_blocks = 0, max_pix = 0;
   for (int i = 0; i < n; ++i) {
-    Parsed P;
-    MRAG_REQUIRE(files[i] != nullptr, "NULL file %d", i);
-    if (!parse(files[i], sizes[i], P)) return mrag::fail(MRAG_ERR_ARG, "jpeg %d unsupported: %s", i, P.why.c_str());
-    Image& im = imgs[i] = P.img;
+    if (!ok[i]) return mrag::fail(MRAG_ERR_ARG, "jpeg %d unsupported: %s", i, P[i].why.c_str());
+    Image& im = imgs[i] = P[i].img;
     im.seg0 = (int32_t)segs.size();
-    im.ecs_off = ecs_total;
     im.coef_off = blocks;
     im.plane_off = planes;
     im.rgb_off = out_offsets[i];
-    for (Segment sg : P.segs) {
-      sg.off = sg.off - P.ecs_begin + ecs_total;
-      sg.img = i;
-      segs.push_back(sg);
+    for (const Segment& sg : P[i].segs) {
+      MRAG_REQUIRE(sg.len < (1ll << 28), "jpeg %d: entropy-coded segment of %lld bytes", i, (long long)sg.len);
+      ParSeg ps;
+      ps.uoff = stage_bytes;
+      ps.nbits = 0;
+      ps.img = i;
+      ps.mcu0 = sg.mcu0;
+      ps.mcus = sg.mcus;
+      segs.push_back(ps);
+      seg_src.push_back(sg.off);
+      seg_len.push_back(sg.len);
+      stage_bytes += (sg.len + 15) / 16 * 16 + 16;  // unstuffed <= raw; zero tail to 16 bytes
     }
-    ecs_at[i] = P.ecs_begin;
-    ecs_total += P.ecs_end - P.ecs_begin;
-    blocks += P.coef_blocks;
-    planes += P.plane_bytes;
-    max_blocks = std::max(max_blocks, P.coef_blocks);
+    blocks += P[i].coef_blocks;
+    planes += P[i].plane_bytes;
+    max_blocks = std::max(max_blocks, P[i].coef_blocks);
     max_pix = std::max(max_pix, (int64_t)im.width * im.height);
   }
-  if (ecs_total + 64 > (int64_t)C.stage_cap) {
-    const size_t cap = std::max<size_t>((size_t)ecs_total + 64, C.stage_cap * 2);
+  if (stage_bytes > (int64_t)C.stage_cap) {
+    const size_t cap = std::max<size_t>((size_t)stage_bytes, C.stage_cap * 2);
     MRAG_HIP(hipStreamSynchronize(s));  // a previous batch's copy may still read the old buffer
     if (C.stage) (void)hipHostFree(C.stage);
     C.stage = nullptr;
@@ -149,21 +256,25 @@ int mrag_jpeg_decode(const uint8_t* const* files, const int64_t* sizes, int32_t 
   }
   // the previous batch's copy out of the staging buffer must be done before it is rewritten
   MRAG_HIP(hipStreamSynchronize(s));
-  for (int i = 0; i < n; ++i) {
-    const int64_t len = (i + 1 < n ? imgs[i + 1].ecs_off : ecs_total) - imgs[i].ecs_off;
-    std::memcpy(C.stage + imgs[i].ecs_off, files[i] + ecs_at[i], (size_t)len);
-  }
-  if (int rc = ensure(C.ecs, (size_t)ecs_total + 64)) return rc;  // Bits reads up to 32 B past a segment
+  parallel([&](int i) {
+    for (int q = imgs[i].seg0, e = imgs[i].seg0 + (int)P[i].segs.size(); q < e; ++q) {
+      uint8_t* dst = C.stage + segs[q].uoff;
+      const int64_t u = unstuff(files[i] + seg_src[q], seg_len[q], dst);
+      std::memset(dst + u, 0, (size_t)((u + 15) / 16 * 16 - u));
+      segs[q].nbits = (uint32_t)(u * 8);
+    }
+  });
+  if (int rc = ensure(C.ecs, (size_t)stage_bytes)) return rc;
   if (int rc = ensure(C.imgs, sizeof(Image) * (size_t)n)) return rc;
-  if (int rc = ensure(C.segs, sizeof(Segment) * segs.size())) return rc;
+  if (int rc = ensure(C.segs, sizeof(ParSeg) * segs.size())) return rc;
   if (int rc = ensure(C.coef, (size_t)blocks * 128)) return rc;
   if (int rc = ensure(C.planes, (size_t)planes)) return rc;
-  MRAG_HIP(hipMemcpyAsync(C.ecs.p, C.stage, (size_t)ecs_total, hipMemcpyHostToDevice, s));
+  MRAG_HIP(hipMemcpyAsync(C.ecs.p, C.stage, (size_t)stage_bytes, hipMemcpyHostToDevice, s));
   MRAG_HIP(hipMemcpyAsync(C.imgs.p, imgs.data(), sizeof(Image) * (size_t)n, hipMemcpyHostToDevice, s));
-  MRAG_HIP(hipMemcpyAsync(C.segs.p, segs.data(), sizeof(Segment) * segs.size(), hipMemcpyHostToDevice, s));
+  MRAG_HIP(hipMemcpyAsync(C.segs.p, segs.data(), sizeof(ParSeg) * segs.size(), hipMemcpyHostToDevice, s));
   MRAG_HIP(hipMemsetAsync(C.coef.p, 0, (size_t)blocks * 128, s));
-  hipLaunchKernelGGL(jpeg_huff_kernel, dim3((unsigned)segs.size()), dim3(1), 0, s, (const Image*)C.imgs.p,
-                     (const Segment*)C.segs.p, (const uint8_t*)C.ecs.p, (int16_t*)C.coef.p);
+  hipLaunchKernelGGL(jpeg_huff_par_kernel, dim3((unsigned)segs.size()), dim3(PAR_LANES), 0, s, (const Image*)C.imgs.p,
+                     (const ParSeg*)C.segs.p, (const uint8_t*)C.ecs.p, (int16_t*)C.coef.p);
   MRAG_CHECK_LAUNCH();
   hipLaunchKernelGGL(jpeg_idct_kernel, dim3((unsigned)((max_blocks + 255) / 256), (unsigned)n), dim3(256), 0, s,
                      (const Image*)C.imgs.p, (const int16_t*)C.coef.p, (uint8_t*)C.planes.p);

@@ -200,6 +200,251 @@ __host__ __device__ inline void decode_block(Bits& br, const Huff& dc, const Huf
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Parallel entropy decoding of one segment (K13a). The segment's bytes are unstuffed on the host
+// (0xFF00 -> 0xFF; the first 0xFF not followed by 0x00 ends the data, as Bits treats it), so a bit
+// position is a plain offset, and zero bits follow the data (Bits feeds zeros there too).
+// The bits are cut into one chunk per lane. The decoder state at a token boundary is
+// (bit position, block of the MCU b, coefficient index k); a token (Huffman code + its extra
+// bits) belongs to the chunk its first bit lies in. Every lane first decodes its chunk from its
+// first bit with a guessed state (b = 0, k = 0) and records its exit (the state at the first token
+// boundary at or past the chunk end) and checkpoints (the state and running counts at the first
+// token boundary past NCP fixed positions). A Huffman stream resynchronises: a decode started at
+// a wrong position soon lands on the true token boundaries with the true (b, k), after which it is
+// the true decode. Then, until no exit changes, every lane whose entry (its predecessor's exit)
+// differs from the state it last decoded from decodes again from that entry, and stops at the
+// first checkpoint whose state it meets (the rest of the chunk is then known); lane 0's entry is
+// exact, so lane i is exact after at most i rounds (in practice one). Block counts and per-component
+// DC-difference sums of each chunk, prefix-summed over the lanes, give every lane its first block
+// and its DC predictors, and a final decode from the exact entries writes the coefficients:
+// the same tokens, the same values, as decode_segment.
+struct PState {
+  uint32_t p;   // bit position of the next token
+  uint32_t bk;  // block of the MCU << 8 | coefficient index (0 = the DC token is next)
+};
+struct PCheck {
+  uint32_t p, bk;
+  int32_t n[4];  // completed blocks, DC-difference sums of components 0..2 since the entry
+};
+constexpr int PAR_NCP = 4;         // checkpoints per chunk
+constexpr int PAR_LANES = 256;     // lanes (chunks) per segment at most
+constexpr int PAR_MIN_BITS = 4096; // shortest chunk
+
+// Per-image tables for the parallel decoder: the four Huffman tables and, per block of the MCU,
+// its component and table ids.
+struct PTabs {
+  Huff h[4];           // dc0, dc1, ac0, ac1
+  uint8_t tdc[8], tac[8], cmp[8];
+  int32_t bpm;
+};
+
+// Component and table ids of every block of the MCU (the Huffman tables are copied separately).
+__host__ __device__ inline void make_ptab_ids(const Image& im, PTabs& T) {
+  int b = 0;
+  for (int c = 0; c < im.ncomp; ++c) {
+    const int nb = im.ncomp == 1 ? 1 : im.comp[c].h * im.comp[c].v;
+    for (int i = 0; i < nb; ++i, ++b) {
+      T.tdc[b] = (uint8_t)im.comp[c].td;
+      T.tac[b] = (uint8_t)(2 + im.comp[c].ta);
+      T.cmp[b] = (uint8_t)c;
+    }
+  }
+  T.bpm = b;
+}
+
+// Lanes and chunk length for a segment of nbits bits; lane t covers [start, end), the last lane
+// to the end of the data; checkpoints at NCP evenly spaced positions inside the chunk.
+__host__ __device__ inline void par_geom(uint32_t nbits, int& nl, uint32_t& chunk) {
+  const uint32_t want = (nbits + PAR_MIN_BITS - 1) / PAR_MIN_BITS;
+  nl = want < 1 ? 1 : (want > (uint32_t)PAR_LANES ? PAR_LANES : (int)want);
+  chunk = (nbits + (uint32_t)nl - 1) / (uint32_t)nl;
+}
+__host__ __device__ inline void par_lane(uint32_t nbits, int nl, uint32_t chunk, int t, uint32_t& start, uint32_t& end,
+                                         uint32_t (&cpos)[PAR_NCP]) {
+  const uint64_t s = (uint64_t)t * chunk;
+  start = s < nbits ? (uint32_t)s : nbits;
+  end = t == nl - 1 ? nbits : (start + chunk < nbits ? start + chunk : nbits);
+  for (int j = 0; j < PAR_NCP; ++j) cpos[j] = start + (uint32_t)((uint64_t)(j + 1) * (end - start) / (PAR_NCP + 1));
+}
+
+// Bit reader over unstuffed bytes (big-endian 32-bit words, 16 bytes per load, the next 16 bytes
+// requested one load ahead; bytes past the data read as zero).
+struct PBits {
+  const uint8_t* base;
+  uint32_t nblk;           // 16-byte blocks holding data (the last one zero-padded)
+  uint32_t blk;            // block of cur
+  uint32_t cur[4], nxt[4];
+  int j;                   // next word of cur
+  uint64_t buf;            // MSB-aligned
+  int cnt;
+  __host__ __device__ static uint32_t bswap(uint32_t x) {
+    return (x >> 24) | ((x >> 8) & 0xFF00u) | ((x << 8) & 0xFF0000u) | (x << 24);
+  }
+  __host__ __device__ void load(uint32_t i, uint32_t (&w)[4]) const {
+    if (i < nblk) {
+      const uint32_t* q = (const uint32_t*)(base + (size_t)i * 16);
+      w[0] = bswap(q[0]);
+      w[1] = bswap(q[1]);
+      w[2] = bswap(q[2]);
+      w[3] = bswap(q[3]);
+    } else {
+      w[0] = w[1] = w[2] = w[3] = 0;
+    }
+  }
+  __host__ __device__ uint32_t take() {
+    const uint32_t w = j == 0 ? cur[0] : j == 1 ? cur[1] : j == 2 ? cur[2] : cur[3];
+    if (++j == 4) {
+      cur[0] = nxt[0];
+      cur[1] = nxt[1];
+      cur[2] = nxt[2];
+      cur[3] = nxt[3];
+      ++blk;
+      load(blk + 1, nxt);
+      j = 0;
+    }
+    return w;
+  }
+  __host__ __device__ void init(const uint8_t* b, uint32_t nbytes, uint32_t p) {
+    base = b;
+    nblk = (nbytes + 15) / 16;
+    blk = p >> 7;
+    load(blk, cur);
+    load(blk + 1, nxt);
+    j = (int)((p >> 5) & 3);
+    const uint64_t w0 = take(), w1 = take();
+    const int sh = (int)(p & 31);
+    buf = ((w0 << 32) | w1) << sh;
+    cnt = 64 - sh;
+  }
+  __host__ __device__ void refill() {
+    if (cnt <= 32) {
+      buf |= (uint64_t)take() << (32 - cnt);
+      cnt += 32;
+    }
+  }
+};
+
+enum { PAR_RECORD = 0, PAR_SYNC = 1, PAR_WRITE = 2 };
+
+// Decode one chunk from state st (updated to the exit) until the next token would start at or
+// past `end`. RECORD: counts since the entry into n, checkpoints cp[j] at the positions cpos[j].
+// SYNC: the same, but on meeting a recorded checkpoint state, n becomes the chunk total implied by
+// the record (tot_old) and the function returns true (exit unchanged; later checkpoints rebased).
+// WRITE: coefficients of blocks g .. (g < gtot) into coef (block g of the segment = MCU
+// mcu0 + g / bpm), DC predictors pred[]; stops early when g reaches gtot.
+template <int MODE, class TAB>
+__host__ __device__ inline bool par_run(const TAB& T, PBits& br, PState& st, uint32_t end, int32_t (&n)[4],
+                                        PCheck* cp, int cstride, const uint32_t* cpos, const int32_t* tot_old,
+                                        const Image* im, int16_t* coef, int64_t g, int64_t gtot, int mcu0,
+                                        int32_t* pred) {
+  uint32_t p = st.p;
+  int b = (int)(st.bk >> 8), k = (int)(st.bk & 255);
+  int jcp = 0;
+  if (MODE != PAR_WRITE)
+    while (jcp < PAR_NCP && cpos[jcp] <= p) ++jcp;  // checkpoints behind the entry are not ours
+  int64_t blk = 0;
+  int my = 0, mx = 0;
+  auto locate = [&]() {
+    const int64_t m = mcu0 + g / T.bpm;
+    my = (int)(m / im->mcux);
+    mx = (int)(m - (int64_t)my * im->mcux);
+    const int c = T.cmp[b];
+    const Comp& kc = im->comp[c];
+    int first = 0;
+    for (int q = 0; q < b; ++q) first += T.cmp[q] == c ? 1 : 0;
+    const int v = first / kc.h, h = first - v * kc.h;
+    blk = kc.coef_off + (int64_t)(my * kc.v + v) * kc.bw + (mx * kc.h + h);
+  };
+  if (MODE == PAR_WRITE) {
+    if (g >= gtot) {
+      st.p = p;
+      return false;
+    }
+    locate();
+  }
+  while (MODE == PAR_WRITE ? (p < end && g < gtot) : p < end) {
+    if (MODE != PAR_WRITE && jcp < PAR_NCP && p >= cpos[jcp]) {
+      PCheck& c = cp[jcp * cstride];
+      const uint32_t bk = (uint32_t)(b << 8 | k);
+      if (MODE == PAR_SYNC && c.p == p && c.bk == bk) {
+        // synchronised: from here on the decode is the recorded one
+        int32_t d[4];
+        for (int q = 0; q < 4; ++q) d[q] = n[q] - c.n[q];
+        for (int q = 0; q < 4; ++q) n[q] = tot_old[q] + d[q];
+        for (int jj = jcp; jj < PAR_NCP; ++jj)
+          for (int q = 0; q < 4; ++q) cp[jj * cstride].n[q] += d[q];
+        return true;
+      }
+      c.p = p;
+      c.bk = bk;
+      for (int q = 0; q < 4; ++q) c.n[q] = n[q];
+      ++jcp;
+    }
+    br.refill();
+    const uint32_t top = (uint32_t)(br.buf >> 32);
+    const Huff& h = T.h[k == 0 ? T.tdc[b] : T.tac[b]];
+    const uint32_t e = h.look(top >> 23);
+    int l, sym;
+    if (e >> 8) {
+      l = (int)(e >> 8);
+      sym = (int)(e & 0xFF);
+    } else {
+      l = 10;
+      int32_t code = (int32_t)(top >> 22);
+      while (l <= 16 && code > h.maxcode[l]) {
+        ++l;
+        code = (int32_t)(top >> (32 - l));
+      }
+      if (l > 16) {  // corrupt code: 16 bits dropped, symbol 0 (as Bits::decode)
+        l = 16;
+        sym = 0;
+      } else {
+        sym = (int)h.val((uint32_t)(code + h.valoff[l]) & 0xFF);
+      }
+    }
+    const int s = k == 0 ? sym : (sym & 15);
+    const uint32_t v = s ? (top << l) >> (32 - s) : 0u;
+    br.buf <<= (l + s);
+    br.cnt -= l + s;
+    p += (uint32_t)(l + s);
+    if (k == 0) {
+      const int diff = extend((int)v, s);
+      const int c = T.cmp[b];
+      if (MODE == PAR_WRITE) {
+        pred[c] += diff;
+        coef[blk * 64] = (int16_t)pred[c];
+      } else {
+        n[1 + c] += diff;
+      }
+      k = 1;
+    } else {
+      const int r = sym >> 4;
+      if (s) {
+        k += r;
+        if (MODE == PAR_WRITE && k < 64) coef[blk * 64 + zigzag(k)] = (int16_t)extend((int)v, s);
+        ++k;
+      } else if (r == 15) {
+        k += 16;
+      } else {
+        k = 64;
+      }
+    }
+    if (k >= 64) {
+      k = 0;
+      b = b + 1 == T.bpm ? 0 : b + 1;
+      if (MODE == PAR_WRITE) {
+        ++g;
+        if (g < gtot) locate();
+      } else {
+        ++n[0];
+      }
+    }
+  }
+  st.p = p;
+  st.bk = (uint32_t)(b << 8 | k);
+  return false;
+}
+
 // islow IDCT of one block (coefficients natural order, quant natural order) -> 8x8 samples with
 // libjpeg's range limiting (index masked to 10 bits, then the post-IDCT table).
 __host__ __device__ inline uint8_t idct_limit(int32_t x) {

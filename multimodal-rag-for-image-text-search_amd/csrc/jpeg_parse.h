@@ -5,6 +5,7 @@
 #pragma once
 
 #include <cstdint>
+#include <array>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -28,10 +29,16 @@ struct Parsed {
   std::string why;  // reason when unsupported
 };
 
-inline bool build_huff(const uint8_t bits[17], const uint8_t* vals, int nvals, Huff& h) {
+// tc: 0 = DC table (symbols are magnitude categories 0..11 for 8-bit data), 1 = AC (run / size,
+// size 0..10); a table with other symbols is refused (the file goes to Pillow), so a token is at
+// most 16 + 11 bits.
+inline bool build_huff(int tc, const uint8_t bits[17], const uint8_t* vals, int nvals, Huff& h) {
   std::memset(&h, 0, sizeof(h));
   if (nvals > 256) return false;
-  for (int i = 0; i < nvals; ++i) h.vals4[i >> 2] |= (uint32_t)vals[i] << ((i & 3) * 8);
+  for (int i = 0; i < nvals; ++i) {
+    if (tc == 0 ? vals[i] > 11 : (vals[i] & 15) > 10) return false;
+    h.vals4[i >> 2] |= (uint32_t)vals[i] << ((i & 3) * 8);
+  }
   int32_t code = 0, k = 0;
   for (int l = 1; l <= 16; ++l) {
     const int n = bits[l];
@@ -115,7 +122,7 @@ inline bool parse(const uint8_t* d, int64_t n, Parsed& P) {
         for (int l = 1; l <= 16; ++l) total += (bits[l] = s[i + l]);
         if (i + 17 + total > sl || tc > 1 || th > 1) return fail(P, "DHT table");
         Huff& h = tc == 0 ? im.dc[th] : im.ac[th];
-        if (!build_huff(bits, s + i + 17, total, h)) return fail(P, "bad Huffman table");
+        if (!build_huff(tc, bits, s + i + 17, total, h)) return fail(P, "bad Huffman table");
         (tc == 0 ? dcset : acset)[th] = true;
         i += 17 + total;
       }
@@ -222,11 +229,14 @@ inline bool parse(const uint8_t* d, int64_t n, Parsed& P) {
   int64_t q = P.ecs_begin, seg_start = P.ecs_begin;
   std::vector<std::pair<int64_t, int64_t>> raw;
   while (true) {
+    // next 0xFF (entropy-coded bytes are mostly not 0xFF: memchr, not a byte loop)
+    const void* f = q < n ? std::memchr(d + q, 0xFF, (size_t)(n - q)) : nullptr;
+    q = f ? (const uint8_t*)f - d : n;
     if (q + 1 >= n) {
       raw.emplace_back(seg_start, n - seg_start);
       break;
     }
-    if (d[q] == 0xFF) {
+    {
       const int b = d[q + 1];
       if (b == 0x00 || b == 0xFF) {
         q += b == 0x00 ? 2 : 1;
@@ -241,7 +251,6 @@ inline bool parse(const uint8_t* d, int64_t n, Parsed& P) {
       raw.emplace_back(seg_start, q - seg_start);
       break;
     }
-    ++q;
   }
   P.ecs_end = raw.back().first + raw.back().second;
   const int64_t per = im.restart > 0 ? im.restart : total_mcus;
@@ -279,6 +288,100 @@ __host__ __device__ inline void decode_segment(const Image& im, const uint8_t* e
         }
     }
   }
+}
+
+// Unstuffed bytes of one segment (K13a's input): 0xFF00 -> 0xFF; the first 0xFF not followed by
+// 0x00 (or last in the segment) ends the data, where Bits starts feeding zeros. Returns the length.
+inline int64_t unstuff(const uint8_t* src, int64_t len, uint8_t* dst) {
+  uint8_t* o = dst;
+  int64_t i = 0;
+  while (i < len) {
+    const void* f = std::memchr(src + i, 0xFF, (size_t)(len - i));
+    const int64_t j = f ? (const uint8_t*)f - src : len;
+    std::memcpy(o, src + i, (size_t)(j - i));
+    o += j - i;
+    if (j >= len) break;
+    if (j + 1 < len && src[j + 1] == 0x00) {
+      *o++ = 0xFF;
+      i = j + 2;
+    } else {
+      break;
+    }
+  }
+  return o - dst;
+}
+
+// Host emulation of K13a over one segment: the kernel's passes, lane by lane, with its barrier
+// semantics (a round reads every exit before any lane rewrites its own). u: unstuffed bytes,
+// readable and zero up to the next multiple of 16. Returns the number of resynchronisation
+// rounds that changed an exit (the kernel runs one more to see that nothing changed). coef: the
+// image's coefficient blocks, as decode_segment takes them.
+inline int decode_segment_par(const Image& im, const uint8_t* u, uint32_t nbytes, int mcu0, int mcus, int16_t* coef) {
+  PTabs T;
+  T.h[0] = im.dc[0];
+  T.h[1] = im.dc[1];
+  T.h[2] = im.ac[0];
+  T.h[3] = im.ac[1];
+  make_ptab_ids(im, T);
+  const uint32_t nbits = nbytes * 8u;
+  int nl;
+  uint32_t chunk;
+  par_geom(nbits, nl, chunk);
+  std::vector<PCheck> cps((size_t)PAR_NCP * PAR_LANES);
+  std::vector<PState> ex(nl), entry(nl), myexit(nl);
+  std::vector<std::array<int32_t, 4>> tot(nl);
+  std::vector<std::array<uint32_t, 4>> cposv(nl);
+  std::vector<uint32_t> endv(nl);
+  for (int t = 0; t < nl; ++t) {
+    uint32_t start, end, cpos[PAR_NCP];
+    par_lane(nbits, nl, chunk, t, start, end, cpos);
+    for (int j = 0; j < PAR_NCP; ++j) cposv[t][j] = cpos[j];
+    endv[t] = end;
+    PBits br;
+    br.init(u, nbytes, start);
+    PState st{start, 0};
+    entry[t] = st;
+    int32_t n[4] = {0, 0, 0, 0};
+    par_run<PAR_RECORD>(T, br, st, end, n, &cps[t], PAR_LANES, cpos, nullptr, &im, nullptr, 0, 0, 0, nullptr);
+    ex[t] = myexit[t] = st;
+    for (int q = 0; q < 4; ++q) tot[t][q] = n[q];
+  }
+  int rounds = 0;
+  while (true) {
+    const std::vector<PState> snap = ex;
+    bool changed = false;
+    for (int t = 1; t < nl; ++t) {
+      const PState e = snap[t - 1];
+      if (e.p == entry[t].p && e.bk == entry[t].bk) continue;
+      entry[t] = e;
+      PState st = e;
+      PBits br;
+      br.init(u, nbytes, e.p);
+      int32_t m[4] = {0, 0, 0, 0};
+      const bool synced = par_run<PAR_SYNC>(T, br, st, endv[t], m, &cps[t], PAR_LANES, cposv[t].data(),
+                                            tot[t].data(), &im, nullptr, 0, 0, 0, nullptr);
+      for (int q = 0; q < 4; ++q) tot[t][q] = m[q];
+      if (!synced && (st.p != myexit[t].p || st.bk != myexit[t].bk)) {
+        myexit[t] = ex[t] = st;
+        changed = true;
+      }
+    }
+    if (!changed) break;
+    ++rounds;
+  }
+  int32_t pre[4] = {0, 0, 0, 0};
+  const int64_t gtot = (int64_t)mcus * T.bpm;
+  for (int t = 0; t < nl; ++t) {
+    PState st = t == 0 ? PState{0, 0} : ex[t - 1];
+    PBits br;
+    br.init(u, nbytes, st.p);
+    int32_t pred[3] = {pre[1], pre[2], pre[3]};
+    int32_t n[4] = {0, 0, 0, 0};
+    par_run<PAR_WRITE>(T, br, st, t == nl - 1 ? 0xFFFFFFFFu : endv[t], n, nullptr, 0, nullptr, nullptr, &im,
+                       coef, pre[0], gtot, mcu0, pred);
+    for (int q = 0; q < 4; ++q) pre[q] += tot[t][q];
+  }
+  return rounds;
 }
 
 }  // namespace mrag_jpeg

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """K13 vs Pillow on the bench's synthetic JPEG files (bench._write_images: 640x480 .. 1024x768,
-q90, 4:2:0): decode img/s of Pillow on the decode pool and of mrag_jpeg_decode (batches of 256,
-bytes already in host memory), and load_batch_device end to end (read + probe + decode + K0)."""
+q90, 4:2:0): decode img/s of Pillow on the decode pool and of mrag_jpeg_decode (256 and 1024 files
+per call, bytes already in host memory), and load_batch_device end to end (read + probe + decode + K0)."""
 import ctypes
 import json
 import os
@@ -31,39 +31,35 @@ try:
     t0 = time.perf_counter()
     arrays = decode_batch(paths)
     res["pillow_pool_img_s"] = round(len(paths) / (time.perf_counter() - t0), 1)
-    offs_all = []
-    for i in range(0, len(paths), 256):
-        sz = np.array([a.size for a in arrays[i:i + 256]], dtype=np.int64)
-        o = np.zeros(len(sz), dtype=np.int64)
-        o[1:] = np.cumsum(sz)[:-1]
-        offs_all.append((o, int(sz.sum())))
     stream = torch.cuda.current_stream(dev).cuda_stream
 
-    def k13():
+    def k13(per):
         outs = []
-        for bi, i in enumerate(range(0, len(paths), 256)):
-            chunk = raw[i:i + 256]
-            o, tot = offs_all[bi]
-            out = torch.empty(tot, dtype=torch.uint8, device=dev)
+        for i in range(0, len(paths), per):
+            chunk = raw[i:i + per]
+            sz = np.array([a.size for a in arrays[i:i + per]], dtype=np.int64)
+            o = np.zeros(len(sz), dtype=np.int64)
+            o[1:] = np.cumsum(sz)[:-1]
+            out = torch.empty(int(sz.sum()), dtype=torch.uint8, device=dev)
             files = (ctypes.c_char_p * len(chunk))(*chunk)
             fsz = np.array([len(b) for b in chunk], dtype=np.int64)
             _native.call("mrag_jpeg_decode", ctypes.cast(files, ctypes.c_void_p), fsz.ctypes.data, len(chunk),
                          out.data_ptr(), o.ctypes.data, 0, stream)
-            outs.append(out)
+            outs.append((i, o, out))
         return outs
 
-    k13()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    outs = k13()
-    torch.cuda.synchronize()
-    res["k13_img_s"] = round(len(paths) / (time.perf_counter() - t0), 1)
     ok = True
-    for bi, i in enumerate(range(0, len(paths), 256)):
-        h = outs[bi].cpu().numpy()
-        o, _ = offs_all[bi]
-        for j, a in enumerate(arrays[i:i + 256]):
-            ok &= bool(np.array_equal(h[o[j]:o[j] + a.size].reshape(a.shape), a))
+    for per in (256, 1024):  # files per launch
+        k13(per)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        outs = k13(per)
+        torch.cuda.synchronize()
+        res[f"k13_img_s_{per}_per_launch"] = round(len(paths) / (time.perf_counter() - t0), 1)
+        for i, o, out in outs:
+            h = out.cpu().numpy()
+            for j, a in enumerate(arrays[i:i + per]):
+                ok &= bool(np.array_equal(h[o[j]:o[j] + a.size].reshape(a.shape), a))
     res["k13_equals_pillow"] = ok
     load_batch_device(paths[:256])
     torch.cuda.synchronize()
