@@ -471,7 +471,7 @@ def ingest_leg(n_images: int = 2048):
     """``embed_images_batch`` over a folder of image files (app/ml/embeddings.py:73-91, the
     ingest path behind index_image_nodes): baseline JPEGs decoded on the GPU (K13, byte-identical
     to Pillow), the PNGs with Pillow on the host thread pool, K0 resize + crop on the GPU,
-    ViT-B/32, L2 normalise; encoder batches of 256, K13 launches of four batches, the next group
+    ViT-B/32, L2 normalise; encoder batches of 256, one K13 launch per batch, the next batch
     prepared on the host while the GPU works on the current one. Reported: img/s of the whole call
     and each stage alone over the same files (and Pillow decoding every file, the host decode K13
     replaces)."""

@@ -24,7 +24,7 @@ import numpy as np
 from app.settings import settings
 
 _TEXT_MODEL: Optional[Any] = None
-_DECODE_GROUP_BATCHES = 4  # encoder batches per K13 decode launch in embed_images_batch
+_DECODE_GROUP_BATCHES = 1  # encoder batches per K13 decode launch (profiles/r5s18_ingest_group_ab.jsonl)
 _CLIP_MODEL: Optional[Any] = None
 _CLIP_PROCESSOR: Optional[Any] = None
 
@@ -109,9 +109,8 @@ def embed_images_batch(paths: Sequence[Path], batch_size: int = 8) -> np.ndarray
     paths = list(paths)
     out: List[np.ndarray] = []
     if native and os.environ.get("MRAG_HOST_RESIZE") != "1":
-        # decode-bound ingest: the host prepares group g + 1 (file reads, Pillow for what K13 does
-        # not take) while the GPU decodes group g's JPEGs in one K13 launch (its time is set by the
-        # largest file, not by the count) and resizes + encodes it batch by batch
+        # the host prepares group g + 1 (file reads, Pillow for what K13 does not take) while the
+        # GPU decodes group g's JPEGs in one K13 launch and resizes + encodes it batch by batch
         from concurrent.futures import ThreadPoolExecutor
 
         group = _DECODE_GROUP_BATCHES * step
