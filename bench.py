@@ -470,7 +470,8 @@ def _write_images(d: str, n: int, seed: int = 9):
 def ingest_leg(n_images: int = 2048):
     """``embed_images_batch`` over a folder of image files (app/ml/embeddings.py:73-91, the
     ingest path behind index_image_nodes): baseline JPEGs decoded on the GPU (K13, byte-identical
-    to Pillow), the PNGs with Pillow on the host thread pool, K0 resize + crop on the GPU,
+    to Pillow), the PNGs inflated on the host thread pool and reconstructed on the GPU (K14), K0
+    resize + crop on the GPU,
     ViT-B/32, L2 normalise; encoder batches of 256, one K13 launch per batch, the next batch
     prepared on the host while the GPU works on the current one. Reported: img/s of the whole call
     and each stage alone over the same files (and Pillow decoding every file, the host decode K13
@@ -498,12 +499,13 @@ def ingest_leg(n_images: int = 2048):
         t_all = time.perf_counter() - t0
         workers = decode_workers()  # the pool embed_images_batch prepares on (app/encoders/preprocess.py)
         group = emb_mod._DECODE_GROUP_BATCHES * 256
-        # the stages alone, over the same files: host prepare (reads, probe, Pillow for the PNGs),
-        # K13 decode of each group's JPEGs (+ the copy of the host-decoded images), K0 per batch, ViT
+        # the stages alone, over the same files: host prepare (reads, probes, the PNGs' inflate),
+        # K13 / K14 decode of each group (+ the copy of any host-decoded image), K0 per batch, ViT
         t0 = time.perf_counter()
         prepared = [prepare_batch(paths[i:i + group]) for i in range(0, len(paths), group)]
         t_prep = time.perf_counter() - t0
-        k13_files = sum(1 for g in prepared for j, _ in g if j is not None)
+        k13_files = sum(1 for g in prepared for j, _ in g if j is not None and j[0] == "jpeg")
+        k14_files = sum(1 for g in prepared for j, _ in g if j is not None and j[0] == "png")
         _sync()
         t0 = time.perf_counter()
         groups = [upload_decode(g) for g in prepared]
@@ -535,11 +537,12 @@ def ingest_leg(n_images: int = 2048):
         "images_per_s": round(n_images / t_all, 1),
         "ms_per_256": round(t_all / n_images * 256 * 1e3, 3),
         "stages_alone_images_per_s": {"host_prepare": round(n_images / t_prep, 1),
-                                      "k13_jpeg_decode_device": round(n_images / t_k13, 1),
+                                      "k13_k14_decode_device": round(n_images / t_k13, 1),
                                       "k0_resize_crop_device": round(n_images / t_rs, 1),
                                       "vit_b32_tower": round(n_images / t_vit, 1),
                                       "pillow_decode_every_file_host": round(n_images / t_pil, 1)},
         "files_decoded_by_k13": k13_files,
+        "files_reconstructed_by_k14": k14_files,
         "decode_group_images": group,
         "decode_threads": workers,
         "unit_rows": ok,

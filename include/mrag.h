@@ -235,6 +235,24 @@ int mrag_jpeg_probe(const uint8_t* data, int64_t size, int32_t* width, int32_t* 
 int mrag_jpeg_decode(const uint8_t* const* files, const int64_t* sizes, int32_t n, uint8_t* out,
                      const int64_t* out_offsets, int32_t device, void* stream);
 
+/* K14: PNG decode with the scanline reconstruction on the GPU, byte-identical to Pillow's decode +
+ * convert("RGB") (the same reference call as K13, for the PNGs it supports: bit depth 8, grey /
+ * grey + alpha / RGB / RGBA, not interlaced, width <= 8192).
+ * mrag_png_probe: host-only chunk parse (CRC-32 checked) of one file; returns 1, the size and the
+ * inflated byte count when K14 decodes it, 0 when the caller must decode it on the host (palette,
+ * 16-bit, interlaced, bad CRC ...), negative on bad arguments.
+ * mrag_png_inflate: host zlib inflate of the IDAT stream into `raw` (cap >= the probe's raw_bytes:
+ * h scanlines of 1 filter byte + w x bpp bytes); *bpp = bytes per pixel (1, 2, 3, 4); returns 1,
+ * 0 when the stream is corrupt or short (decode that file on the host), negative on bad arguments.
+ * Thread-safe, no device work: call it from decode threads.
+ * mrag_png_unfilter: n inflated images (host raws, dims = n x {w, h, bpp}) reconstructed and
+ * converted into device memory `out`, image i as H x W x 3 u8 RGB at out_offsets[i] (host array).
+ * Synchronous on `stream`. */
+int mrag_png_probe(const uint8_t* data, int64_t size, int32_t* width, int32_t* height, int64_t* raw_bytes);
+int mrag_png_inflate(const uint8_t* data, int64_t size, uint8_t* raw, int64_t cap, int32_t* bpp);
+int mrag_png_unfilter(const uint8_t* const* raws, const int32_t* dims, int32_t n, uint8_t* out,
+                      const int64_t* out_offsets, int32_t device, void* stream);
+
 /* K3 building block: C[M][N] (op)= A[M][K] . W[N][K]^T + bias (device pointers;
  * A, W fp16 row-major; epilogue 0 f16 out, 1 f16 quick_gelu, 2 f16 gelu_erf,
  * 3 f32 C += , 4 f32 out). N % 128 == 0, K % 64 == 0; bias and C 16-byte aligned. */

@@ -47,6 +47,10 @@ SIGNATURES = {
                                         ctypes.POINTER(_c_int), _c_int, _c_int, _vp, _vp]),
     "mrag_jpeg_probe": (_c_int, [ctypes.c_char_p, _c_i64, ctypes.POINTER(_c_int), ctypes.POINTER(_c_int)]),
     "mrag_jpeg_decode": (_c_int, [_vp, _vp, _c_int, _vp, _vp, _c_int, _vp]),
+    "mrag_png_probe": (_c_int, [ctypes.c_char_p, _c_i64, ctypes.POINTER(_c_int), ctypes.POINTER(_c_int),
+                                ctypes.POINTER(_c_i64)]),
+    "mrag_png_inflate": (_c_int, [ctypes.c_char_p, _c_i64, _vp, _c_i64, ctypes.POINTER(_c_int)]),
+    "mrag_png_unfilter": (_c_int, [_vp, _vp, _c_int, _vp, _vp, _c_int, _vp]),
 }
 
 _lib: Optional[ctypes.CDLL] = None

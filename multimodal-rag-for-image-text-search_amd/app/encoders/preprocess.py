@@ -4,10 +4,12 @@ the GPU patch-embed kernel.
 
 Two implementations with identical bytes: ``load_batch_device`` (the default for the
 native encoders) decodes baseline JPEGs on the GPU (``mrag_jpeg_decode``, K13 in csrc/jpeg.hip —
-libjpeg-turbo's decode as Pillow runs it, restated), every other file on host threads with
-Pillow, and runs the resize + crop on the GPU (``mrag_image_resize_crop``, K0 in
-csrc/imgprep.hip — Pillow's fixed-point resampler restated); ``load_batch`` does all of it with
-PIL on the host. ``MRAG_HOST_DECODE=1`` decodes every file on the host (A/B timing).
+libjpeg-turbo's decode as Pillow runs it, restated), 8-bit grey / RGB(A) PNGs by a zlib inflate on
+host threads and the scanline reconstruction on the GPU (``mrag_png_unfilter``, K14 in
+csrc/png.hip), every other file on host threads with Pillow, and runs the resize + crop on the
+GPU (``mrag_image_resize_crop``, K0 in csrc/imgprep.hip — Pillow's fixed-point resampler
+restated); ``load_batch`` does all of it with PIL on the host. ``MRAG_HOST_DECODE=1`` decodes
+every file on the host (A/B timing).
 
 Restates CLIPImageProcessor's PIL path (the processor the reference loads for
 openai/clip-vit-base-patch32, app/ml/embeddings.py:39-43, 84-85):
@@ -152,26 +154,39 @@ def decode_batch(items: Sequence[Union[str, Path, Image.Image]]) -> List[np.ndar
     return list(_pool().map(decode_rgb, items))
 
 
+_PNG_SIG = b"\x89PNG\r\n\x1a\n"
+
+
 def _prepare_one(x):
-    """A file K13 decodes on the GPU -> (bytes, (h, w)), None; anything else (a PIL image, a PNG,
-    a progressive JPEG ...) -> None, its u8 HxWx3 RGB decoded here with Pillow."""
+    """The host half for one item: a JPEG K13 decodes -> ("jpeg", file bytes, (h, w), 0), None; a
+    PNG K14 reconstructs -> ("png", inflated scanlines, (h, w), bytes per pixel), None; anything
+    else (a PIL image, a palette or 16-bit PNG, a progressive JPEG ...) -> None, its u8 HxWx3 RGB
+    decoded here with Pillow."""
     if isinstance(x, Image.Image):
         return None, decode_rgb(x)
     with open(x, "rb") as f:
         b = f.read()
-    if b[:2] == b"\xff\xd8" and os.environ.get("MRAG_HOST_DECODE") != "1":
+    if os.environ.get("MRAG_HOST_DECODE") != "1":
         from app import _native
 
         w, h = ctypes.c_int32(0), ctypes.c_int32(0)
-        if _native.load().mrag_jpeg_probe(b, len(b), ctypes.byref(w), ctypes.byref(h)) == 1:
-            return (b, (h.value, w.value)), None
+        if b[:2] == b"\xff\xd8":
+            if _native.load().mrag_jpeg_probe(b, len(b), ctypes.byref(w), ctypes.byref(h)) == 1:
+                return ("jpeg", b, (h.value, w.value), 0), None
+        elif b[:8] == _PNG_SIG:
+            lib, nraw = _native.load(), ctypes.c_int64(0)
+            if lib.mrag_png_probe(b, len(b), ctypes.byref(w), ctypes.byref(h), ctypes.byref(nraw)) == 1:
+                raw = np.empty(nraw.value, dtype=np.uint8)
+                bpp = ctypes.c_int32(0)
+                if lib.mrag_png_inflate(b, len(b), raw.ctypes.data, nraw.value, ctypes.byref(bpp)) == 1:
+                    return ("png", raw, (h.value, w.value), bpp.value), None
     with Image.open(io.BytesIO(b)) as im:
         return None, np.asarray(im.convert("RGB"), dtype=np.uint8)
 
 
 def prepare_batch(items: Sequence[Union[str, Path, Image.Image]]) -> list:
     """The host half of ``load_batch_device`` on the process-wide pool: file bytes of the JPEGs the
-    GPU decodes, Pillow arrays of everything else (embed_images_batch runs it for the next batch
+    GPU decodes, inflated scanlines of the PNGs it reconstructs, Pillow arrays of everything else (embed_images_batch runs it for the next batch
     while the GPU works on the current one)."""
     return list(_pool().map(_prepare_one, items)) if len(items) else []
 
@@ -188,11 +203,8 @@ class DeviceImages:
 
 
 def upload_decode(prepared: list, device: int = 0) -> DeviceImages:
-    """The device half's decode: K13 decodes the group's JPEGs straight into one pixel buffer and
-    the host-decoded images are copied in after them (one pinned copy). K13 decodes every file
-    of a launch in parallel (one wave per entropy-coded segment) at the pace of the largest, so a
-    larger group costs about the same time: embed_images_batch decodes several encoder batches
-    per launch."""
+    """The device half's decode into one pixel buffer: the host-decoded images (one pinned copy),
+    then K13's JPEGs and K14's PNGs, each kind in one launch."""
     import torch
 
     from app import _native
@@ -202,13 +214,14 @@ def upload_decode(prepared: list, device: int = 0) -> DeviceImages:
     for j, a in prepared:
         if a is not None and (a.ndim != 3 or a.shape[2] != 3):
             raise ValueError(f"expected HxWx3 u8 images, got shape {a.shape}")
-    dims = np.array([j[1] if j is not None else a.shape[:2] for j, a in prepared], dtype=np.int64).reshape(n, 2)
+    dims = np.array([j[2] if j is not None else a.shape[:2] for j, a in prepared], dtype=np.int64).reshape(n, 2)
     sizes = dims[:, 0] * dims[:, 1] * 3
     host = [i for i in range(n) if prepared[i][1] is not None]
-    jpeg = [i for i in range(n) if prepared[i][0] is not None]
-    offsets = np.zeros(n, dtype=np.int64)  # host-decoded images first (one contiguous copy), then K13's
+    jpeg = [i for i in range(n) if prepared[i][0] is not None and prepared[i][0][0] == "jpeg"]
+    png = [i for i in range(n) if prepared[i][0] is not None and prepared[i][0][0] == "png"]
+    offsets = np.zeros(n, dtype=np.int64)  # host-decoded images first (one contiguous copy), then K13's, K14's
     pos = 0
-    for i in host + jpeg:
+    for i in host + jpeg + png:
         offsets[i] = pos
         pos += int(sizes[i])
     pix = torch.empty(max(pos, 1), dtype=torch.uint8, device=dev)
@@ -222,10 +235,17 @@ def upload_decode(prepared: list, device: int = 0) -> DeviceImages:
                 sv[offsets[i]:offsets[i] + sizes[i]] = np.ascontiguousarray(prepared[i][1], dtype=np.uint8).reshape(-1)
             pix[:nh].copy_(staging, non_blocking=True)
         if jpeg:
-            files = (ctypes.c_char_p * len(jpeg))(*[prepared[i][0][0] for i in jpeg])
-            fsz = np.array([len(prepared[i][0][0]) for i in jpeg], dtype=np.int64)
+            files = (ctypes.c_char_p * len(jpeg))(*[prepared[i][0][1] for i in jpeg])
+            fsz = np.array([len(prepared[i][0][1]) for i in jpeg], dtype=np.int64)
             offs = np.ascontiguousarray(offsets[jpeg])
             _native.call("mrag_jpeg_decode", ctypes.cast(files, ctypes.c_void_p), fsz.ctypes.data, len(jpeg),
+                         pix.data_ptr(), offs.ctypes.data, device, stream)
+        if png:
+            raws = (ctypes.c_void_p * len(png))(*[prepared[i][0][1].ctypes.data for i in png])
+            pdims = np.array([[prepared[i][0][2][1], prepared[i][0][2][0], prepared[i][0][3]] for i in png],
+                             dtype=np.int32)
+            offs = np.ascontiguousarray(offsets[png])
+            _native.call("mrag_png_unfilter", ctypes.cast(raws, ctypes.c_void_p), pdims.ctypes.data, len(png),
                          pix.data_ptr(), offs.ctypes.data, device, stream)
     return DeviceImages(pix, offsets, dims)
 
@@ -256,11 +276,11 @@ def resize_images(imgs: DeviceImages, start: int = 0, count: int = -1, device: i
 
 
 def upload_resize(prepared: list, device: int = 0, size: int = SIZE):
-    """The whole device half: decode (K13 + host copies), then K0 -> u8 [n, size, size, 3]."""
+    """The whole device half: decode (K13, K14, host copies), then K0 -> u8 [n, size, size, 3]."""
     return resize_images(upload_decode(prepared, device=device), device=device, size=size)
 
 
 def load_batch_device(items: Sequence[Union[str, Path, Image.Image]], device: int = 0):
-    """Decode (baseline JPEG on the GPU, the rest on the host thread pool), resize + crop on the
-    GPU: u8 [n, 224, 224, 3] CUDA tensor."""
+    """Decode (baseline JPEG on the GPU, PNG reconstruction on the GPU after a host inflate, the rest
+    on the host thread pool), resize + crop on the GPU: u8 [n, 224, 224, 3] CUDA tensor."""
     return upload_resize(prepare_batch(items), device=device)

@@ -181,7 +181,7 @@ Ctx g_ctx[64];
 extern "C" {
 
 int mrag_jpeg_probe(const uint8_t* data, int64_t size, int32_t* width, int32_t* height) {
-  MRAG_REQUIRE(data && width && height && size >= 0, "NULL argument");
+  if (!data || !width || !height || size < 0) return -mrag::fail(MRAG_ERR_ARG, "NULL argument");  // not 1
   Parsed P;
   if (!parse(data, size, P)) {
     *width = *height = 0;

@@ -79,9 +79,9 @@ def test_load_batch_device_mixed_equals_host(cuda, tmp_path):
 
 
 def test_embed_images_batch_groups_equal_host_decode(cuda, tmp_path):
-    """embed_images_batch over 600 files (JPEG + PNG; two K13 groups of 4 x 256, the second
-    partial): the embeddings equal those of the all-host decode (MRAG_HOST_DECODE=1) bit for bit,
-    since the 224x224 inputs are byte-identical."""
+    """embed_images_batch over 600 files (JPEG for K13 + PNG for K14; decode groups of 256, the
+    last partial): the embeddings equal those of the all-host decode (MRAG_HOST_DECODE=1) bit for
+    bit, since the 224x224 inputs are byte-identical."""
     from PIL import Image
 
     from app.ml import embeddings as emb
