@@ -493,10 +493,13 @@ def ingest_leg(n_images: int = 2048):
         nbytes = sum(os.path.getsize(p) for p in paths)
         emb_mod.embed_images_batch(paths[:256])  # warm: model + workspaces
         _sync()
-        t0 = time.perf_counter()
-        out = emb_mod.embed_images_batch(paths)
-        _sync()
-        t_all = time.perf_counter() - t0
+        calls = []  # the first full call also grows the pinned staging buffers; then two more
+        for _ in range(3):
+            t0 = time.perf_counter()
+            out = emb_mod.embed_images_batch(paths)
+            _sync()
+            calls.append(time.perf_counter() - t0)
+        t_all = sorted(calls)[1]
         workers = decode_workers()  # the pool embed_images_batch prepares on (app/encoders/preprocess.py)
         group = emb_mod._DECODE_GROUP_BATCHES * 256
         # the stages alone, over the same files: host prepare (reads, probes, the PNGs' inflate),
@@ -536,6 +539,7 @@ def ingest_leg(n_images: int = 2048):
     return {
         "images_per_s": round(n_images / t_all, 1),
         "ms_per_256": round(t_all / n_images * 256 * 1e3, 3),
+        "calls_images_per_s": [round(n_images / t, 1) for t in calls],
         "stages_alone_images_per_s": {"host_prepare": round(n_images / t_prep, 1),
                                       "k13_k14_decode_device": round(n_images / t_k13, 1),
                                       "k0_resize_crop_device": round(n_images / t_rs, 1),
@@ -547,7 +551,8 @@ def ingest_leg(n_images: int = 2048):
         "decode_threads": workers,
         "unit_rows": ok,
         "workload": f"{n_images} synthetic files (3/4 JPEG q90, 1/4 PNG; 640x480 .. 1024x768; "
-                    f"{nbytes / 1e6:.1f} MB on disk), embed_images_batch(paths) in batches of 256",
+                    f"{nbytes / 1e6:.1f} MB on disk), embed_images_batch(paths) in batches of 256; "
+                    f"images_per_s = median of three calls",
     }
 
 

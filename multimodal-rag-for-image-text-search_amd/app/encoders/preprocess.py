@@ -204,7 +204,8 @@ class DeviceImages:
 
 def upload_decode(prepared: list, device: int = 0) -> DeviceImages:
     """The device half's decode into one pixel buffer: the host-decoded images (one pinned copy),
-    then K13's JPEGs and K14's PNGs, each kind in one launch."""
+    then K13's JPEGs and K14's PNGs, each kind in one launch, on the calling thread's current
+    stream; the pixels are complete when it returns (any stream may read them)."""
     import torch
 
     from app import _native
@@ -247,6 +248,8 @@ def upload_decode(prepared: list, device: int = 0) -> DeviceImages:
             offs = np.ascontiguousarray(offsets[png])
             _native.call("mrag_png_unfilter", ctypes.cast(raws, ctypes.c_void_p), pdims.ctypes.data, len(png),
                          pix.data_ptr(), offs.ctypes.data, device, stream)
+        if host and not (jpeg or png):  # K13 / K14 return complete; a lone copy must be too
+            torch.cuda.current_stream(dev).synchronize()
     return DeviceImages(pix, offsets, dims)
 
 

@@ -109,22 +109,49 @@ def embed_images_batch(paths: Sequence[Path], batch_size: int = 8) -> np.ndarray
     paths = list(paths)
     out: List[np.ndarray] = []
     if native and os.environ.get("MRAG_HOST_RESIZE") != "1":
-        # the host prepares group g + 1 (file reads, Pillow for what K13 does not take) while the
-        # GPU decodes group g's JPEGs in one K13 launch and resizes + encodes it batch by batch
+        # three stages in flight: the host prepares group g + 2 (file reads, probes, PNG inflate,
+        # Pillow for what the GPU decoders do not take), a second thread decodes group g + 1 on the
+        # GPU (K13 / K14, its own stream), and this thread resizes (K0) and encodes group g
         from concurrent.futures import ThreadPoolExecutor
+
+        import torch
 
         group = _DECODE_GROUP_BATCHES * step
         starts = list(range(0, len(paths), group))
-        with ThreadPoolExecutor(max_workers=1) as ahead:
-            nxt = ahead.submit(processor.decode, paths[0:group])
-            for i, start in enumerate(starts):
-                prepared = nxt.result()
-                if i + 1 < len(starts):
-                    nxt = ahead.submit(processor.decode, paths[starts[i + 1]:starts[i + 1] + group])
-                imgs = processor.decode_device(prepared)
-                for c0 in range(0, len(prepared), step):
+        from app.encoders.models import _device_index
+
+        dstream = torch.cuda.Stream(torch.device("cuda", _device_index()))
+
+        with ThreadPoolExecutor(max_workers=1) as prep_ex, ThreadPoolExecutor(max_workers=1) as dec_ex:
+            preps = {}
+            decs = {}
+
+            def prep(i):
+                if i < len(starts) and i not in preps:
+                    preps[i] = prep_ex.submit(processor.decode, paths[starts[i]:starts[i] + group])
+
+            def dec(i):
+                if i < len(starts) and i not in decs:
+                    prep(i)
+                    fut = preps[i]
+
+                    def run():
+                        prepared = fut.result()
+                        with torch.cuda.stream(dstream):
+                            return len(prepared), processor.decode_device(prepared)
+
+                    decs[i] = dec_ex.submit(run)
+
+            for i in range(len(starts)):
+                dec(i)
+                dec(i + 1)
+                prep(i + 2)
+                n_i, imgs = decs.pop(i).result()
+                preps.pop(i, None)
+                for c0 in range(0, n_i, step):
                     inputs = processor.from_device(imgs, c0, step)
                     out.append(_to_numpy(model.get_image_features(**_kwargs(inputs))))
+                del imgs
         return _normalize(np.vstack(out))
     for start in range(0, len(paths), step):
         batch_paths = paths[start:start + step]

@@ -15,7 +15,9 @@
 //
 // Layout: images are u8 RGB HWC, concatenated (byte offsets); output u8 [n][size][size][3],
 // which mrag_encoder_embed_images consumes (normalise + patchify fused there).
+#include <array>
 #include <cmath>
+#include <map>
 #include <mutex>
 #include <vector>
 
@@ -91,24 +93,53 @@ __device__ __forceinline__ uint8_t clip8(int v) {
   return (uint8_t)(s < 0 ? 0 : (s > 255 ? 255 : s));
 }
 
-// pass 1: rows [y0, y0 + nrows) of image blockIdx.y, crop columns -> tmp [nrows][size][3]
+// pass 1: rows [y0, y0 + nrows) of image blockIdx.y, crop columns -> tmp [nrows][size][3].
+// Block: RH_ROWS source rows; thread: one output pixel (its three channels share each tap). The
+// image's column tap table is staged in LDS when it fits (RH_LDS ints), else read from global.
+// Each channel sums its taps in Pillow's order into an int32 (exact in any order anyway).
+constexpr int RH_ROWS = 8;
+constexpr int RH_LDS = 6144;
+
 __global__ __launch_bounds__(256) void resize_h_kernel(const uint8_t* __restrict__ px, const ImgPlan* __restrict__ plans,
                                                        const int32_t* __restrict__ coef, uint8_t* __restrict__ tmp,
                                                        int size) {
+  __shared__ int32_t stab[RH_LDS];
   const ImgPlan pl = plans[blockIdx.y];
-  const int r = blockIdx.x;
-  if (r >= pl.nrows) return;
-  const uint8_t* src = px + pl.src_off + (int64_t)(pl.y0 + r) * pl.w * 3;
-  uint8_t* dst = tmp + pl.tmp_off + (int64_t)r * size * 3;
+  const int r0 = blockIdx.x * RH_ROWS;
+  if (r0 >= pl.nrows) return;  // whole block
   const int stride = 2 + pl.hk;
-  for (int t = threadIdx.x; t < size * 3; t += blockDim.x) {
-    const int x = t / 3, c = t - 3 * (t / 3);
-    const int32_t* e = coef + pl.hoff + x * stride;
-    const int xmin = e[0], n = e[1];
-    int ss = 1 << (PRECISION_BITS - 1);
-    for (int j = 0; j < n; ++j) ss += (int)src[(xmin + j) * 3 + c] * e[2 + j];
-    dst[t] = clip8(ss);
-  }
+  const int nt = size * stride;
+  const int32_t* gtab = coef + pl.hoff;
+  const bool in_lds = nt <= RH_LDS;
+  if (in_lds)
+    for (int i = threadIdx.x; i < nt; i += blockDim.x) stab[i] = gtab[i];
+  __syncthreads();
+  auto rows = [&](const int32_t* tab) {
+    for (int t = threadIdx.x; t < RH_ROWS * size; t += blockDim.x) {
+      const int rr = t / size, x = t - rr * size, r = r0 + rr;
+      if (r >= pl.nrows) break;
+      const uint8_t* sp = px + pl.src_off + (int64_t)(pl.y0 + r) * pl.w * 3;
+      const int32_t* e = tab + x * stride;
+      const int xmin = e[0], n = e[1];
+      sp += xmin * 3;
+      int s0 = 1 << (PRECISION_BITS - 1), s1 = s0, s2 = s0;
+#pragma unroll 4
+      for (int j = 0; j < n; ++j) {
+        const int c = e[2 + j];
+        s0 += (int)sp[3 * j] * c;
+        s1 += (int)sp[3 * j + 1] * c;
+        s2 += (int)sp[3 * j + 2] * c;
+      }
+      uint8_t* d = tmp + pl.tmp_off + ((int64_t)r * size + x) * 3;
+      d[0] = clip8(s0);
+      d[1] = clip8(s1);
+      d[2] = clip8(s2);
+    }
+  };
+  if (in_lds)
+    rows(stab);
+  else
+    rows(gtab);
 }
 
 // pass 2: crop row blockIdx.x of image blockIdx.y from the pass-1 rows -> out [size][size][3]
@@ -126,6 +157,29 @@ __global__ __launch_bounds__(256) void resize_v_kernel(const ImgPlan* __restrict
     for (int j = 0; j < n; ++j) ss += (int)src[(int64_t)(ymin + j) * size * 3 + t] * e[2 + j];
     dst[t] = clip8(ss);
   }
+}
+
+// Tap tables depend only on (in size, out size, first output, count): images of one size share
+// them. A process-wide cache of the tables computed so far (bounded; cleared when full), so a
+// batch computes only the sizes it has not met before.
+using TapKey = std::array<int, 4>;
+struct TapTable {
+  std::vector<int32_t> tab;  // rows of [xmin, n, taps ...]
+  int k;                     // taps per row
+};
+std::mutex g_tap_mu;
+std::map<TapKey, TapTable> g_taps;
+
+TapTable taps(int in_size, int out_size, int o0, int cnt) {
+  const TapKey key{in_size, out_size, o0, cnt};
+  std::lock_guard<std::mutex> lk(g_tap_mu);
+  auto it = g_taps.find(key);
+  if (it != g_taps.end()) return it->second;
+  if (g_taps.size() >= 4096) g_taps.clear();
+  TapTable t;
+  t.k = out_size != in_size ? coeffs(in_size, out_size, o0, cnt, t.tab) : identity(o0, cnt, t.tab);
+  g_taps.emplace(key, t);
+  return t;
 }
 
 // grow-only device workspace (per process; calls are serialised by `mu`)
@@ -149,6 +203,33 @@ extern "C" int mrag_image_resize_crop(const uint8_t* pixels, const int64_t* offs
   std::vector<int32_t> coef;
   int64_t tmp_bytes = 0;
   int max_rows = 0;
+  // tables of this call, one copy per distinct key: offset, taps, and for row tables the source
+  // rows the crop reads (the table is stored relative to its first row)
+  struct Placed {
+    int32_t off, k, y0, nrows;
+  };
+  std::map<TapKey, Placed> placed_h, placed_v;
+  auto place = [&](std::map<TapKey, Placed>& m, int in_size, int out_size, int o0, bool rows) -> Placed {
+    const TapKey key{in_size, out_size, o0, size};
+    auto it = m.find(key);
+    if (it != m.end()) return it->second;
+    TapTable t = taps(in_size, out_size, o0, size);
+    Placed p{(int32_t)coef.size(), t.k, 0, 0};
+    if (rows) {
+      int y0 = 1 << 30, y1 = 0;
+      for (int y = 0; y < size; ++y) {
+        const int32_t* e = &t.tab[(size_t)y * (2 + t.k)];
+        y0 = std::min(y0, (int)e[0]);
+        y1 = std::max(y1, (int)(e[0] + e[1]));
+      }
+      for (int y = 0; y < size; ++y) t.tab[(size_t)y * (2 + t.k)] -= y0;
+      p.y0 = y0;
+      p.nrows = y1 - y0;
+    }
+    coef.insert(coef.end(), t.tab.begin(), t.tab.end());
+    m.emplace(key, p);
+    return p;
+  };
   for (int i = 0; i < n; ++i) {
     const int w = widths[i], h = heights[i];
     MRAG_REQUIRE(w > 0 && h > 0 && offsets[i] >= 0, "image %d: bad size %dx%d / offset", i, w, h);
@@ -161,20 +242,14 @@ extern "C" int mrag_image_resize_crop(const uint8_t* pixels, const int64_t* offs
     pl.src_off = offsets[i];
     pl.w = w;
     pl.h = h;
-    pl.hoff = (int32_t)coef.size();
-    pl.hk = nw != w ? coeffs(w, nw, left, size, coef) : identity(left, size, coef);
-    pl.voff = (int32_t)coef.size();
-    pl.vk = nh != h ? coeffs(h, nh, top, size, coef) : identity(top, size, coef);
-    // rows of the source the crop reads, then make the row windows relative to them
-    int y0 = 1 << 30, y1 = 0;
-    for (int y = 0; y < size; ++y) {
-      const int32_t* e = &coef[(size_t)pl.voff + (size_t)y * (2 + pl.vk)];
-      y0 = std::min(y0, (int)e[0]);
-      y1 = std::max(y1, (int)(e[0] + e[1]));
-    }
-    for (int y = 0; y < size; ++y) coef[(size_t)pl.voff + (size_t)y * (2 + pl.vk)] -= y0;
-    pl.y0 = y0;
-    pl.nrows = y1 - y0;
+    const Placed ph = place(placed_h, w, nw, left, false);
+    const Placed pv = place(placed_v, h, nh, top, true);
+    pl.hoff = ph.off;
+    pl.hk = ph.k;
+    pl.voff = pv.off;
+    pl.vk = pv.k;
+    pl.y0 = pv.y0;
+    pl.nrows = pv.nrows;
     pl.tmp_off = tmp_bytes;
     tmp_bytes += ((int64_t)pl.nrows * size * 3 + 255) / 256 * 256;
     max_rows = std::max(max_rows, pl.nrows);
@@ -199,7 +274,7 @@ extern "C" int mrag_image_resize_crop(const uint8_t* pixels, const int64_t* offs
   char* ws = (char*)g_ws.p;
   MRAG_HIP(hipMemcpyAsync(ws, plans.data(), plan_bytes, hipMemcpyHostToDevice, s));
   MRAG_HIP(hipMemcpyAsync(ws + coef_off, coef.data(), coef.size() * 4, hipMemcpyHostToDevice, s));
-  hipLaunchKernelGGL(resize_h_kernel, dim3((unsigned)max_rows, (unsigned)n), dim3(256), 0, s, pixels,
+  hipLaunchKernelGGL(resize_h_kernel, dim3((unsigned)((max_rows + RH_ROWS - 1) / RH_ROWS), (unsigned)n), dim3(256), 0, s, pixels,
                      (const ImgPlan*)ws, (const int32_t*)(ws + coef_off), (uint8_t*)(ws + tmp_off), size);
   MRAG_CHECK_LAUNCH();
   hipLaunchKernelGGL(resize_v_kernel, dim3((unsigned)size, (unsigned)n), dim3(256), 0, s, (const ImgPlan*)ws,

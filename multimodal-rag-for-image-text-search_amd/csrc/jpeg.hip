@@ -13,8 +13,9 @@
 //                           single-lane workgroup per segment: 70-78 ms per launch, the largest
 //                           file's serial chain).
 //   K13b jpeg_idct_kernel   one thread per 8x8 block: dequantise + islow IDCT into the planes.
-//   K13c jpeg_color_kernel  one thread per output pixel: fancy chroma upsampling + YCbCr -> RGB,
-//                           H x W x 3 u8 at the caller's offset (the layout K0 resizes from).
+//   K13c jpeg_color_kernel  one thread per four pixels of a row: fancy chroma upsampling +
+//                           YCbCr -> RGB, H x W x 3 u8 at the caller's offset (the layout K0
+//                           resizes from), 12 bytes per store.
 // Files K13 does not support (progressive, arithmetic, CMYK, 4:4:0, tiny chroma) are reported by
 // mrag_jpeg_probe and decoded on the host by the caller, as the reference decodes everything.
 #include <algorithm>
@@ -138,18 +139,23 @@ __global__ __launch_bounds__(256) void jpeg_idct_kernel(const Image* __restrict_
   }
 }
 
+// K13c: four consecutive pixels of a row per thread, their 12 RGB bytes in one store
 __global__ __launch_bounds__(256) void jpeg_color_kernel(const Image* __restrict__ imgs,
                                                          const uint8_t* __restrict__ planes, uint8_t* __restrict__ out) {
   const Image& im = imgs[blockIdx.y];
+  const int qw = (im.width + 3) / 4;  // quads per row
   const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (p >= (int64_t)im.width * im.height) return;
-  const int y = (int)(p / im.width), x = (int)(p - (int64_t)y * im.width);
-  uint8_t rgb[3];
-  color_pixel(im, planes + im.plane_off, x, y, rgb);
-  uint8_t* o = out + im.rgb_off + p * 3;
-  o[0] = rgb[0];
-  o[1] = rgb[1];
-  o[2] = rgb[2];
+  if (p >= (int64_t)qw * im.height) return;
+  const int y = (int)(p / qw), x0 = (int)(p - (int64_t)y * qw) * 4;
+  uint8_t rgb[12];
+  const int nx = im.width - x0 < 4 ? im.width - x0 : 4;
+  for (int q = 0; q < nx; ++q) color_pixel(im, planes + im.plane_off, x0 + q, y, rgb + 3 * q);
+  uint8_t* o = out + im.rgb_off + ((int64_t)y * im.width + x0) * 3;
+  if (nx == 4) {
+    __builtin_memcpy(o, rgb, 12);
+  } else {
+    for (int i = 0; i < 3 * nx; ++i) o[i] = rgb[i];
+  }
 }
 
 struct DevBuf {
@@ -219,7 +225,7 @@ int mrag_jpeg_decode(const uint8_t* const* files, const int64_t* sizes, int32_t 
   std::vector<ParSeg> segs;
   std::vector<int64_t> seg_src;  // raw segment start in its file
   std::vector<int64_t> seg_len;
-  int64_t stage_bytes = 0, blocks = 0, planes = 0, max_blocks = 0, max_pix = 0;
+  int64_t stage_bytes = 0, blocks = 0, planes = 0, max_blocks = 0, max_quads = 0;
   for (int i = 0; i < n; ++i) {
     if (!ok[i]) return mrag::fail(MRAG_ERR_ARG, "jpeg %d unsupported: %s", i, P[i].why.c_str());
     Image& im = imgs[i] = P[i].img;
@@ -243,7 +249,7 @@ int mrag_jpeg_decode(const uint8_t* const* files, const int64_t* sizes, int32_t 
     blocks += P[i].coef_blocks;
     planes += P[i].plane_bytes;
     max_blocks = std::max(max_blocks, P[i].coef_blocks);
-    max_pix = std::max(max_pix, (int64_t)im.width * im.height);
+    max_quads = std::max(max_quads, (int64_t)(im.width + 3) / 4 * im.height);
   }
   if (stage_bytes > (int64_t)C.stage_cap) {
     const size_t cap = std::max<size_t>((size_t)stage_bytes, C.stage_cap * 2);
@@ -279,7 +285,7 @@ int mrag_jpeg_decode(const uint8_t* const* files, const int64_t* sizes, int32_t 
   hipLaunchKernelGGL(jpeg_idct_kernel, dim3((unsigned)((max_blocks + 255) / 256), (unsigned)n), dim3(256), 0, s,
                      (const Image*)C.imgs.p, (const int16_t*)C.coef.p, (uint8_t*)C.planes.p);
   MRAG_CHECK_LAUNCH();
-  hipLaunchKernelGGL(jpeg_color_kernel, dim3((unsigned)((max_pix + 255) / 256), (unsigned)n), dim3(256), 0, s,
+  hipLaunchKernelGGL(jpeg_color_kernel, dim3((unsigned)((max_quads + 255) / 256), (unsigned)n), dim3(256), 0, s,
                      (const Image*)C.imgs.p, (const uint8_t*)C.planes.p, out);
   MRAG_CHECK_LAUNCH();
   // the descriptors above live on this host stack frame: the copies must finish before return

@@ -455,14 +455,17 @@ __host__ __device__ inline uint8_t idct_limit(int32_t x) {
   return (uint8_t)(idx - 896);
 }
 
-__host__ __device__ inline void idct_islow(const int16_t* coef, const uint16_t* q, uint8_t* out, int64_t stride) {
+__host__ __device__ inline void idct_islow(const int16_t* coef_g, const uint16_t* q, uint8_t* out, int64_t stride) {
   constexpr int CB = 13, P1 = 2;
+  int16_t coef[64];  // the block in registers: eight 16-byte loads, not 64 two-byte ones
+  __builtin_memcpy(coef, coef_g, sizeof(coef));
   // libjpeg's JLONG is 64-bit on LP64 hosts: the products are formed in int64 and the pass-1
   // results truncated to int, as its workspace is
   typedef int64_t L;
   constexpr L F0298 = 2446, F0390 = 3196, F0541 = 4433, F0765 = 6270, F0899 = 7373, F1175 = 9633, F1501 = 12299,
               F1847 = 15137, F1961 = 16069, F2053 = 16819, F2562 = 20995, F3072 = 25172;
   int32_t ws[64];
+#pragma unroll
   for (int c = 0; c < 8; ++c) {
     const int16_t* in = coef + c;
     const uint16_t* qq = q + c;
@@ -514,13 +517,15 @@ __host__ __device__ inline void idct_islow(const int16_t* coef, const uint16_t* 
     ws[3 * 8 + c] = (int32_t)((tmp13 + tmp0 + RD) >> SH);
     ws[4 * 8 + c] = (int32_t)((tmp13 - tmp0 + RD) >> SH);
   }
+#pragma unroll
   for (int r = 0; r < 8; ++r) {
     const int32_t* w = ws + r * 8;
-    uint8_t* o = out + r * stride;
+    uint8_t o[8];  // one 8-byte store per row
     if (w[1] == 0 && w[2] == 0 && w[3] == 0 && w[4] == 0 && w[5] == 0 && w[6] == 0 && w[7] == 0) {
       constexpr int SH0 = P1 + 3;
       const uint8_t v = idct_limit((int32_t)(((L)w[0] + ((L)1 << (SH0 - 1))) >> SH0));
       for (int c = 0; c < 8; ++c) o[c] = v;
+      __builtin_memcpy(out + r * stride, o, 8);
       continue;
     }
     L z2 = w[2], z3 = w[6];
@@ -563,6 +568,7 @@ __host__ __device__ inline void idct_islow(const int16_t* coef, const uint16_t* 
     o[5] = idct_limit((int32_t)((tmp12 - tmp1 + RD) >> SH));
     o[3] = idct_limit((int32_t)((tmp13 + tmp0 + RD) >> SH));
     o[4] = idct_limit((int32_t)((tmp13 - tmp0 + RD) >> SH));
+    __builtin_memcpy(out + r * stride, o, 8);
   }
 }
 
