@@ -1,8 +1,8 @@
 """Drop-in for the reference's ``app/ml/retrieve.py``.
 
 ``retrieve_text`` / ``retrieve_images`` (:41-100): cache -> query embeddings (both
-towers, :120-129) -> GPU flat search -> per-hit chunk lookup -> result dicts in score
-order. ``retrieve`` (:103-117): optional cross-encoder rerank + z-score fusion
+towers, :120-129) -> GPU flat search -> chunk lookup of the hits (one SQLite statement for all
+of them when the store has ``get_chunks``) -> result dicts in score order. ``retrieve`` (:103-117): optional cross-encoder rerank + z-score fusion
 (:132-195). Module globals ``_LANCEDB_STORE``, ``_METADATA_STORE``,
 ``embed_text_batch``, ``embed_query_for_images``, ``_get_cross_encoder``,
 ``get_index_version`` are looked up at call time (test seams, tests/test_retrieve.py).
@@ -125,6 +125,18 @@ def _get_embeddings(query: str) -> Tuple[np.ndarray, np.ndarray]:
     return text_vec[0], image_vec
 
 
+def _chunks_for(hits: List[Dict[str, Any]]) -> List[Optional[Chunk]]:
+    """The chunk of every hit, in hit order (reference: one ``get_chunk`` per hit, :55-56 / :88):
+    one batched lookup when the store offers ``get_chunks`` (the drop-in's SQLite store), else
+    per hit (a store without it, e.g. the tests' stand-ins)."""
+    store = _METADATA_STORE
+    many = getattr(store, "get_chunks", None)
+    if many is None or len(hits) < 2:
+        return [store.get_chunk(h["chunk_id"]) for h in hits]
+    found = many([h["chunk_id"] for h in hits])
+    return [found.get(h["chunk_id"]) for h in hits]
+
+
 def retrieve_text(user_id: str, query: str, top_k: Optional[int] = None) -> List[Dict[str, Any]]:
     top_k = top_k or settings.retrieval.index_topk_text
     version = get_index_version(user_id)
@@ -135,8 +147,8 @@ def retrieve_text(user_id: str, query: str, top_k: Optional[int] = None) -> List
     if text_vec.size == 0:
         return []
     results: List[Dict[str, Any]] = []
-    for entry in _LANCEDB_STORE.search_text(user_id, text_vec.tolist(), top_k):
-        chunk = _METADATA_STORE.get_chunk(entry["chunk_id"])
+    hits = _LANCEDB_STORE.search_text(user_id, text_vec.tolist(), top_k)
+    for entry, chunk in zip(hits, _chunks_for(hits)):
         if not chunk or not chunk.text:
             continue
         results.append({"chunk_id": chunk.id, "modality": "text", "score": float(entry["score"]),
@@ -155,8 +167,8 @@ def retrieve_images(user_id: str, query: str, top_k: Optional[int] = None) -> Li
     if image_vec.size == 0:
         return []
     results: List[Dict[str, Any]] = []
-    for entry in _LANCEDB_STORE.search_image(user_id, image_vec.tolist(), top_k):
-        chunk = _METADATA_STORE.get_chunk(entry["chunk_id"])
+    hits = _LANCEDB_STORE.search_image(user_id, image_vec.tolist(), top_k)
+    for entry, chunk in zip(hits, _chunks_for(hits)):
         if not chunk:
             continue
         results.append({"chunk_id": chunk.id, "modality": "image", "score": float(entry["score"]),

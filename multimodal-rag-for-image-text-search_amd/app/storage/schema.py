@@ -102,6 +102,22 @@ class MetadataStore:
         data["meta"] = json.loads(data.get("meta") or "{}")
         return Chunk(**data)
 
+    def get_chunks(self, chunk_ids: List[str]) -> Dict[str, Chunk]:
+        """``get_chunk`` for many ids in one statement per 500 ids (one retrieval's hits): id ->
+        Chunk for the ids present, the same objects ``get_chunk`` builds."""
+        rows = []
+        with self._lock:
+            c = self._c()
+            for i in range(0, len(chunk_ids), 500):
+                part = chunk_ids[i:i + 500]
+                rows += c.execute(f"SELECT * FROM chunks WHERE id IN ({','.join('?' * len(part))})", part).fetchall()
+        out = {}
+        for row in rows:
+            data = {k: row[k] for k in _COLS}
+            data["meta"] = json.loads(data.get("meta") or "{}")
+            out[data["id"]] = Chunk(**data)
+        return out
+
     def list_chunks(self, document_id: str) -> List[Chunk]:
         with self._lock:
             rows = self._c().execute("SELECT * FROM chunks WHERE document_id = ?", (document_id,)).fetchall()

@@ -369,3 +369,31 @@ def test_fuse_scores_matches_reference_fusion():
             got.append(f"t{p}" if p < kt else f"i{p - kt}")
         assert got == [e["chunk_id"] for e in ref], q
         np.testing.assert_array_equal(comb[q][: len(ref)], [e["combined_score"] for e in ref])
+
+
+def test_batched_chunk_lookup_equals_per_hit(tmp_path):
+    """retrieve's hit lookup (one SQLite statement through MetadataStore.get_chunks) returns what the
+    reference's per-hit get_chunk does, in hit order: missing ids -> None, duplicates repeated,
+    more than one statement's worth of ids."""
+    from app.ml import retrieve as r
+    from app.storage.schema import Chunk, MetadataStore
+
+    store = MetadataStore(str(tmp_path / "m.sqlite3"))
+    store.upsert_chunks([Chunk(id=f"c{i}", document_id="d", modality="text" if i % 3 else "image",
+                               text=None if i % 7 == 0 else f"t{i}", page_no=i, meta={"k": i}) for i in range(1200)])
+
+    class PerHit:
+        def get_chunk(self, chunk_id):
+            return store.get_chunk(chunk_id)
+
+    hits = [{"chunk_id": f"c{i}"} for i in [5, 1199, 3, 5, 77, 4000, 0, *range(100, 1150)]]
+    old = r._METADATA_STORE
+    try:
+        r._METADATA_STORE = store
+        batched = r._chunks_for(hits)
+        r._METADATA_STORE = PerHit()
+        per_hit = r._chunks_for(hits)
+    finally:
+        r._METADATA_STORE = old
+    assert [c.model_dump() if c else None for c in batched] == [c.model_dump() if c else None for c in per_hit]
+    assert batched[5] is None and batched[0] is not None
