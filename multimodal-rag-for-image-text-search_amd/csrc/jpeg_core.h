@@ -83,6 +83,10 @@ struct Bits {
   uint64_t w0, w1, x0, x1;
   uint64_t buf;
   int32_t cnt;
+  int64_t data_bits, used;  // bits of real data put in buf / bits consumed
+  bool at_end;              // the data has ended (a marker or the segment end): zeros follow
+  // libjpeg's insufficient_data: a token took bits past the end of the data
+  __host__ __device__ bool insufficient() const { return at_end && used > data_bits; }
   __host__ __device__ void load16(int64_t at, uint64_t& a, uint64_t& b) const {
 #if defined(__HIP_DEVICE_COMPILE__)
     // device: the decoder is wave-uniform, so the window comes through the scalar cache; the
@@ -105,6 +109,8 @@ struct Bits {
     load16(16, x0, x1);
     buf = 0;
     cnt = 0;
+    data_bits = used = 0;
+    at_end = false;
   }
   __host__ __device__ uint32_t byte_at(int64_t rel) {  // rel: at most 2 past the last call's
     const int64_t a = off0 + rel;
@@ -128,13 +134,18 @@ struct Bits {
           const uint32_t b2 = pos + 1 < n ? byte_at(pos + 1) : 0xD9u;
           if (b2 == 0x00) {
             pos += 2;
+            data_bits += 8;
           } else {
             b = 0;  // marker: stay on it, zeros from here
             n = pos;
+            at_end = true;
           }
         } else {
           ++pos;
+          data_bits += 8;
         }
+      } else {
+        at_end = true;
       }
       buf |= (uint64_t)b << (56 - cnt);
       cnt += 8;
@@ -144,6 +155,7 @@ struct Bits {
   __host__ __device__ void skip(int k) {
     buf <<= k;
     cnt -= k;
+    used += k;
   }
   __host__ __device__ uint32_t get(int k) {  // k <= 16, after fill()
     if (k == 0) return 0;
@@ -304,8 +316,10 @@ struct PBits {
     }
     return w;
   }
+  uint32_t nblk_bits;      // bits of data (8 x bytes)
   __host__ __device__ void init(const uint8_t* b, uint32_t nbytes, uint32_t p) {
     base = b;
+    nblk_bits = nbytes * 8u;
     nblk = (nbytes + 15) / 16;
     blk = p >> 7;
     load(blk, cur);
@@ -362,6 +376,8 @@ __host__ __device__ inline bool par_run(const TAB& T, PBits& br, PState& st, uin
     }
     locate();
   }
+  const uint32_t nbits = br.nblk_bits;  // end of the data (WRITE: libjpeg's insufficient_data rule)
+  bool crossed = false;
   while (MODE == PAR_WRITE ? (p < end && g < gtot) : p < end) {
     if (MODE != PAR_WRITE && jcp < PAR_NCP && p >= cpos[jcp]) {
       PCheck& c = cp[jcp * cstride];
@@ -407,6 +423,7 @@ __host__ __device__ inline bool par_run(const TAB& T, PBits& br, PState& st, uin
     br.buf <<= (l + s);
     br.cnt -= l + s;
     p += (uint32_t)(l + s);
+    if (MODE == PAR_WRITE && p > nbits) crossed = true;
     if (k == 0) {
       const int diff = extend((int)v, s);
       const int c = T.cmp[b];
@@ -434,6 +451,9 @@ __host__ __device__ inline bool par_run(const TAB& T, PBits& br, PState& st, uin
       b = b + 1 == T.bpm ? 0 : b + 1;
       if (MODE == PAR_WRITE) {
         ++g;
+        // a token of this MCU needed bits past the data: libjpeg completes the MCU with zero
+        // bits and leaves the rest of the segment zero (jdhuff.c insufficient_data)
+        if (crossed && b == 0) break;
         if (g < gtot) locate();
       } else {
         ++n[0];

@@ -232,10 +232,9 @@ inline bool parse(const uint8_t* d, int64_t n, Parsed& P) {
     // next 0xFF (entropy-coded bytes are mostly not 0xFF: memchr, not a byte loop)
     const void* f = q < n ? std::memchr(d + q, 0xFF, (size_t)(n - q)) : nullptr;
     q = f ? (const uint8_t*)f - d : n;
-    if (q + 1 >= n) {
-      raw.emplace_back(seg_start, n - seg_start);
-      break;
-    }
+    // the file ends inside the entropy-coded data (no marker after it, not even EOI): Pillow
+    // raises "image file is truncated" for such a file, so it is left to Pillow
+    if (q + 1 >= n) return fail(P, "truncated: the file ends inside the entropy-coded data");
     {
       const int b = d[q + 1];
       if (b == 0x00 || b == 0xFF) {
@@ -243,6 +242,9 @@ inline bool parse(const uint8_t* d, int64_t n, Parsed& P) {
         continue;
       }
       if (b >= 0xD0 && b <= 0xD7) {
+        // libjpeg expects RST0, RST1, ... in turn and resynchronises otherwise (jdmarker.c
+        // read_restart_marker / jpeg_resync_to_restart): a file out of that order goes to Pillow
+        if (im.restart > 0 && (b & 7) != (int)(raw.size() & 7)) return fail(P, "restart marker out of order");
         raw.emplace_back(seg_start, q - seg_start);
         q += 2;
         seg_start = q;
@@ -255,7 +257,7 @@ inline bool parse(const uint8_t* d, int64_t n, Parsed& P) {
   P.ecs_end = raw.back().first + raw.back().second;
   const int64_t per = im.restart > 0 ? im.restart : total_mcus;
   const int64_t nseg = (total_mcus + per - 1) / per;
-  if ((int64_t)raw.size() < nseg) return fail(P, "missing restart markers");
+  if (im.restart > 0 ? (int64_t)raw.size() != nseg : raw.size() < 1) return fail(P, "restart intervals != markers");
   P.segs.clear();
   for (int64_t i = 0; i < nseg; ++i) {
     Segment sg;
@@ -287,6 +289,9 @@ __host__ __device__ inline void decode_segment(const Image& im, const uint8_t* e
           decode_block(br, im.dc[k.td], im.ac[k.ta], pred[c], coef + blk * 64);
         }
     }
+    // libjpeg (jdhuff.c): once a token needed bits past the data (insufficient_data), the MCU is
+    // completed with zero bits and the rest of the segment is left zero
+    if (br.insufficient()) break;
   }
 }
 

@@ -56,6 +56,24 @@ def _cmyk(a: np.ndarray) -> bytes:
     return buf.getvalue()
 
 
+def damaged_cases():
+    """(name, bytes) of damaged files: cut inside the entropy-coded data and closed with EOI (libjpeg
+    finishes the MCU in progress with zero bits and leaves the rest zero), cut with nothing after
+    (Pillow raises "image file is truncated"), an RST0 / RST7 spliced in (in a restart-interval
+    file: out of order, libjpeg resynchronises), for plain and restart-interval files."""
+    out = []
+    for seed, (h, w, sub, kw) in enumerate([(480, 640, 2, {}), (301, 223, 0, {}), (480, 640, 1, {"restart_marker_rows": 1}),
+                                            (200, 300, 2, {"restart_marker_blocks": 3})]):
+        b = jpeg_bytes(photo(h, w, 50 + seed), quality=90, subsampling=sub, **kw)
+        for frac in (0.1, 0.5, 0.95, 0.999):
+            cut = int(len(b) * frac)
+            out.append((f"f{seed}_cut{frac}_eoi", b[:cut] + b"\xff\xd9"))
+            out.append((f"f{seed}_cut{frac}", b[:cut]))
+            out.append((f"f{seed}_rst0_at{frac}", b[:cut] + b"\xff\xd0" + b[cut:]))
+            out.append((f"f{seed}_rst7_at{frac}", b[:cut] + b"\xff\xd7" + b[cut:]))
+    return out
+
+
 def pillow_rgb(b: bytes) -> np.ndarray:
     with Image.open(io.BytesIO(b)) as im:
         return np.asarray(im.convert("RGB"), dtype=np.uint8)

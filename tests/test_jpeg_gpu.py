@@ -10,7 +10,7 @@ import os
 import numpy as np
 import pytest
 
-from _jpeg_cases import photo, pillow_rgb, supported_cases, unsupported_cases
+from _jpeg_cases import damaged_cases, photo, pillow_rgb, supported_cases, unsupported_cases
 
 pytestmark = pytest.mark.gpu
 
@@ -100,3 +100,24 @@ def test_embed_images_batch_groups_equal_host_decode(cuda, tmp_path):
     finally:
         del os.environ["MRAG_HOST_DECODE"]
     np.testing.assert_array_equal(gpu, host)
+
+
+def test_damaged_files_as_pillow(cuda, tmp_path):
+    """Damaged JPEGs through load_batch_device: the ones Pillow decodes give the all-host path's
+    bytes (K13 for those it takes, Pillow for the rest); one Pillow refuses raises, as it does in
+    the reference's embed_images_batch."""
+    from app.encoders.preprocess import load_batch, load_batch_device
+
+    ok, refused = [], []
+    for i, (name, b) in enumerate(damaged_cases()):
+        p = tmp_path / f"{i}_{name}.jpg"
+        p.write_bytes(b)
+        try:
+            pillow_rgb(b)
+            ok.append(str(p))
+        except OSError:
+            refused.append(str(p))
+    np.testing.assert_array_equal(load_batch_device(ok).cpu().numpy(), load_batch(ok))
+    assert refused
+    with pytest.raises(OSError):
+        load_batch_device(ok[:3] + refused[:1])
