@@ -12,6 +12,7 @@
 #include <utility>
 #include <vector>
 
+#include "inflate.h"
 #include "png_core.h"
 
 namespace mrag_png {
@@ -76,9 +77,8 @@ inline bool png_parse(const uint8_t* d, int64_t n, PngParsed& P, bool check_crc)
   return true;
 }
 
-// Inflate the IDAT stream into raw (P.raw_bytes bytes). False when the stream is corrupt or ends
-// early, or a scanline's filter byte is not 0..4 (the caller then lets Pillow decode the file).
-inline bool png_inflate(const uint8_t* d, const PngParsed& P, uint8_t* raw) {
+// Inflate the IDAT stream into raw with zlib (the reference implementation of the format).
+inline bool png_inflate_zlib(const uint8_t* d, const PngParsed& P, uint8_t* raw) {
   z_stream z;
   std::memset(&z, 0, sizeof(z));
   if (inflateInit(&z) != Z_OK) return false;
@@ -93,8 +93,8 @@ inline bool png_inflate(const uint8_t* d, const PngParsed& P, uint8_t* raw) {
       z.avail_out = out_take;
       const int rc = inflate(&z, Z_NO_FLUSH);
       left -= out_take - z.avail_out;
-      if (left == 0) {  // every scanline inflated (trailing data is ignored, as Pillow does)
-        ok = true;
+      if (left == 0) {  // every scanline inflated; an error zlib found after them (a bad code, the
+        ok = rc == Z_OK || rc == Z_STREAM_END || rc == Z_BUF_ERROR;  // Adler-32) is one for Pillow too
         stop = true;
         break;
       }
@@ -105,7 +105,24 @@ inline bool png_inflate(const uint8_t* d, const PngParsed& P, uint8_t* raw) {
     }
   }
   inflateEnd(&z);
-  if (!ok) return false;
+  return ok;
+}
+
+// Inflate the IDAT stream into raw (P.raw_bytes bytes): the IDAT data concatenated and inflated by
+// fast_inflate (inflate.h), zlib when that reports an error (so a stream is refused only when
+// zlib refuses it). False when the stream is corrupt or ends early, or a scanline's filter byte is
+// not 0..4 (the caller then lets Pillow decode the file).
+inline bool png_inflate(const uint8_t* d, const PngParsed& P, uint8_t* raw) {
+  static thread_local std::vector<uint8_t> z;
+  size_t n = 0;
+  for (const auto& c : P.idat) n += (size_t)c.second;
+  z.resize(n);
+  size_t o = 0;
+  for (const auto& c : P.idat) {
+    std::memcpy(z.data() + o, d + c.first, (size_t)c.second);
+    o += (size_t)c.second;
+  }
+  if (!fast_inflate(z.data(), n, raw, (size_t)P.raw_bytes) && !png_inflate_zlib(d, P, raw)) return false;
   const int64_t stride = 1 + (int64_t)P.width * P.bpp;
   for (int64_t r = 0; r < P.height; ++r)
     if (raw[r * stride] > 4) return false;

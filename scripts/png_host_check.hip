@@ -22,3 +22,23 @@ extern "C" int png_host_decode(const uint8_t* d, int64_t n, uint8_t* rgb, int64_
   unfilter_rgb_host(raw.data(), P.width, P.height, P.bpp, rgb);
   return 1;
 }
+
+// fast_inflate alone (tests compare it with Python's zlib): 1 when out_len bytes were produced.
+extern "C" int png_fast_inflate(const uint8_t* in, int64_t in_len, uint8_t* out, int64_t out_len) {
+  return fast_inflate(in, (size_t)in_len, out, (size_t)out_len) ? 1 : 0;
+}
+
+// zlib's inflate of the same stream into out (timing comparison)
+extern "C" int png_zlib_inflate(const uint8_t* in, int64_t in_len, uint8_t* out, int64_t out_len) {
+  z_stream z;
+  std::memset(&z, 0, sizeof(z));
+  if (inflateInit(&z) != Z_OK) return 0;
+  z.next_in = const_cast<Bytef*>(in);
+  z.avail_in = (uInt)in_len;
+  z.next_out = out;
+  z.avail_out = (uInt)out_len;
+  const int rc = inflate(&z, Z_NO_FLUSH);
+  const bool ok = z.avail_out == 0 && (rc == Z_OK || rc == Z_STREAM_END || rc == Z_BUF_ERROR);
+  inflateEnd(&z);
+  return ok ? 1 : 0;
+}

@@ -96,3 +96,65 @@ def test_library_probe_and_inflate():
     jpeg = b"\xff\xd8\xff\xe0" + b"\0" * 32
     assert lib.mrag_png_probe(jpeg, len(jpeg), ctypes.byref(w), ctypes.byref(h), ctypes.byref(nraw)) == 0
     assert lib.mrag_png_probe(None, 0, ctypes.byref(w), ctypes.byref(h), ctypes.byref(nraw)) < 0
+
+
+def test_fast_inflate_equals_zlib(host_check):
+    """K14's host inflate (csrc/inflate.h) against Python's zlib: every clean stream (levels 0-9,
+    every strategy, whole and partial outputs) gives zlib's bytes, and on corrupted or truncated
+    streams it accepts exactly what zlib accepts (zlib asked for the same number of bytes, as
+    Pillow asks it for the image's scanlines), with the same bytes."""
+    lib = host_check
+    lib.png_fast_inflate.argtypes = [ctypes.c_char_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64]
+    rng = np.random.default_rng(0)
+
+    def fast(s, n):
+        out = np.zeros(n + 16, np.uint8)
+        return out[:n].tobytes() if lib.png_fast_inflate(s, len(s), out.ctypes.data, n) == 1 else None
+
+    def ref(s, n):
+        try:
+            o = zlib.decompressobj().decompress(s, n)
+            return o if len(o) == n else None
+        except zlib.error:
+            return None
+
+    datas = []
+    for i in range(18):
+        n = int(rng.integers(1, 120000))
+        kind = i % 6
+        if kind == 0:
+            d = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        elif kind == 1:
+            d = rng.integers(0, 4, n, dtype=np.uint8).tobytes()
+        elif kind == 2:
+            d = (b"abcabcabd" * (n // 9 + 1))[:n]
+        elif kind == 3:
+            d = np.repeat(rng.integers(0, 256, n // 50 + 1, dtype=np.uint8), 50)[:n].tobytes()
+        elif kind == 4:
+            d = bytes(n)
+        else:
+            d = np.cumsum(rng.integers(-2, 3, n)).astype(np.uint8).tobytes()
+        datas.append(d)
+    strategies = [zlib.Z_DEFAULT_STRATEGY, zlib.Z_FILTERED, zlib.Z_HUFFMAN_ONLY, zlib.Z_RLE, zlib.Z_FIXED]
+    for d in datas:
+        for lvl in (0, 1, 6, 9):
+            for st in strategies:
+                c = zlib.compressobj(lvl, zlib.DEFLATED, 15, 8, st)
+                s = c.compress(d) + c.flush()
+                for n in (len(d), max(1, len(d) // 2)):
+                    assert fast(s, n) == ref(s, n), (len(d), lvl, st, n)
+    agree = 0
+    for t in range(1500):
+        d = datas[t % len(datas)]
+        c = zlib.compressobj(int(rng.integers(0, 10)), zlib.DEFLATED, 15, 8, strategies[t % 5])
+        s = bytearray(c.compress(d) + c.flush())
+        for _ in range(int(rng.integers(1, 4))):
+            s[int(rng.integers(0, len(s)))] ^= 1 << int(rng.integers(0, 8))
+        if t % 7 == 0:
+            s = s[:int(rng.integers(2, len(s) + 1))]
+        s = bytes(s)
+        n = len(d) if t % 3 else max(1, len(d) - int(rng.integers(0, 100)))
+        f, r = fast(s, n), ref(s, n)
+        assert f == r, t
+        agree += f is not None
+    assert agree > 200  # corrupted streams zlib still decodes are exercised too
