@@ -31,8 +31,8 @@ inline bool png_fail(PngParsed& P, const char* why) {
   return false;
 }
 
-// Parse one file; true when K14 decodes it. check_crc: verify every chunk's CRC-32 (the probe
-// does; a file with a bad CRC goes to Pillow, which decides what it is).
+// Parse one file; true when K14 decodes it. check_crc: verify the CRC-32 of every chunk but IDAT
+// (the probe does; a file with a bad one goes to Pillow, which raises for it).
 inline bool png_parse(const uint8_t* d, int64_t n, PngParsed& P, bool check_crc) {
   static const uint8_t sig[8] = {0x89, 'P', 'N', 'G', 0x0D, 0x0A, 0x1A, 0x0A};
   if (n < 8 || std::memcmp(d, sig, 8) != 0) return png_fail(P, "not a PNG");
@@ -43,7 +43,9 @@ inline bool png_parse(const uint8_t* d, int64_t n, PngParsed& P, bool check_crc)
     const uint8_t* type = d + pos + 4;
     if (len > 0x7fffffff || pos + 12 + len > n) return png_fail(P, "truncated chunk");
     const uint8_t* data = d + pos + 8;
-    if (check_crc) {
+    // Pillow checks the CRC of every chunk it reads except IDAT (PngImageFile.load_read skips
+    // those four bytes): the same here, so a file goes to Pillow exactly when Pillow would raise
+    if (check_crc && std::memcmp(type, "IDAT", 4) != 0) {
       const uint32_t crc = (uint32_t)crc32(crc32(0L, Z_NULL, 0), type, (uInt)(4 + len));
       if (crc != be32(data + len)) return png_fail(P, "bad CRC");
     }

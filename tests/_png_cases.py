@@ -96,9 +96,22 @@ def unsupported_cases():
     Image.fromarray(a[..., 0] > 128).save(bw, "PNG")
     good = png_bytes(a, "RGB")
     bad_crc = bytearray(good)
-    bad_crc[40] ^= 0x55  # inside the first IDAT's data
+    bad_crc[40] ^= 0x55  # the chunk type after IHDR: an unknown chunk with a bad CRC
     return [("palette", b_pal.getvalue()), ("gray16", b16.getvalue()), ("bilevel", bw.getvalue()),
             ("bad_crc", bytes(bad_crc))]
+
+
+def bad_idat_crc_case():
+    """A PNG whose IDAT chunk CRC is wrong but whose data is intact: Pillow does not check IDAT
+    CRCs and decodes it, so K14 takes it too."""
+    a = photo(40, 50, 9)
+    good = bytearray(png_bytes(a, "RGB"))
+    pos = 8
+    while good[pos + 4:pos + 8] != b"IDAT":
+        pos += 12 + int.from_bytes(good[pos:pos + 4], "big")
+    n = int.from_bytes(good[pos:pos + 4], "big")
+    good[pos + 8 + n] ^= 0xFF  # first byte of that chunk's CRC
+    return bytes(good)
 
 
 def truncated_stream_case():

@@ -9,7 +9,7 @@ import os
 import numpy as np
 import pytest
 
-from _png_cases import filtered_png, pillow_rgb, supported_cases, unsupported_cases
+from _png_cases import bad_idat_crc_case, filtered_png, pillow_rgb, supported_cases, unsupported_cases
 
 pytestmark = pytest.mark.gpu
 
@@ -79,6 +79,7 @@ def test_load_batch_device_png_mix_equals_host(cuda, tmp_path):
     items = []
     sup = [c for c in supported_cases() if c[0].startswith(("photo480x640", "noise201x300", "filters300x201"))]
     left = [c for c in unsupported_cases() if c[0] != "bad_crc"]  # Pillow refuses that one itself
+    sup.append(("bad_idat_crc", bad_idat_crc_case()))  # Pillow skips IDAT CRCs: K14 takes it
     for i, (name, b) in enumerate(sup + left):
         p = tmp_path / f"{i}_{name}.png"
         p.write_bytes(b)
