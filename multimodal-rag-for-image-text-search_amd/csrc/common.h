@@ -59,6 +59,23 @@ inline int wait_null_stream(hipEvent_t ev, hipStream_t s) {
   return MRAG_OK;
 }
 
+// Wait for everything queued on s with the calling thread asleep (an event created with
+// hipEventBlockingSync), not spinning: for the multi-millisecond image decode / resize calls,
+// whose host threads share the process's CPU quota with the decode pool.
+inline int blocking_wait(hipStream_t s) {
+  thread_local hipEvent_t ev = nullptr;
+  thread_local int ev_dev = -1;
+  int dev = 0;
+  MRAG_HIP(hipGetDevice(&dev));
+  if (ev == nullptr || ev_dev != dev) {
+    MRAG_HIP(hipEventCreateWithFlags(&ev, hipEventBlockingSync | hipEventDisableTiming));
+    ev_dev = dev;
+  }
+  MRAG_HIP(hipEventRecord(ev, s));
+  MRAG_HIP(hipEventSynchronize(ev));
+  return MRAG_OK;
+}
+
 // Drains a stream on scope exit unless disarmed: an error return after the first launch must not
 // hand buffers that queued kernels still use back to a pool (or drop the lock guarding them).
 struct StreamDrain {

@@ -281,6 +281,6 @@ extern "C" int mrag_image_resize_crop(const uint8_t* pixels, const int64_t* offs
                      (const int32_t*)(ws + coef_off), (const uint8_t*)(ws + tmp_off), out, size);
   MRAG_CHECK_LAUNCH();
   // the host-side plan / coefficient vectors must outlive their copies
-  MRAG_HIP(hipStreamSynchronize(s));
+  if (int rc = mrag::blocking_wait(s)) return rc;
   return MRAG_OK;
 }

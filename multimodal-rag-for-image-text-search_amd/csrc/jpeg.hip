@@ -253,7 +253,7 @@ int mrag_jpeg_decode(const uint8_t* const* files, const int64_t* sizes, int32_t 
   }
   if (stage_bytes > (int64_t)C.stage_cap) {
     const size_t cap = std::max<size_t>((size_t)stage_bytes, C.stage_cap * 2);
-    MRAG_HIP(hipStreamSynchronize(s));  // a previous batch's copy may still read the old buffer
+    if (int rc = mrag::blocking_wait(s)) return rc;  // a previous batch's copy may still read the old buffer
     if (C.stage) (void)hipHostFree(C.stage);
     C.stage = nullptr;
     C.stage_cap = 0;
@@ -261,7 +261,7 @@ int mrag_jpeg_decode(const uint8_t* const* files, const int64_t* sizes, int32_t 
     C.stage_cap = cap;
   }
   // the previous batch's copy out of the staging buffer must be done before it is rewritten
-  MRAG_HIP(hipStreamSynchronize(s));
+  if (int rc = mrag::blocking_wait(s)) return rc;
   parallel([&](int i) {
     for (int q = imgs[i].seg0, e = imgs[i].seg0 + (int)P[i].segs.size(); q < e; ++q) {
       uint8_t* dst = C.stage + segs[q].uoff;
@@ -289,7 +289,7 @@ int mrag_jpeg_decode(const uint8_t* const* files, const int64_t* sizes, int32_t 
                      (const Image*)C.imgs.p, (const uint8_t*)C.planes.p, out);
   MRAG_CHECK_LAUNCH();
   // the descriptors above live on this host stack frame: the copies must finish before return
-  MRAG_HIP(hipStreamSynchronize(s));
+  if (int rc = mrag::blocking_wait(s)) return rc;
   return MRAG_OK;
 }
 

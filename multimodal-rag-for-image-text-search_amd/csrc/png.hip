@@ -225,14 +225,14 @@ int mrag_png_unfilter(const uint8_t* const* raws, const int32_t* dims, int32_t n
   hipStream_t s = (hipStream_t)stream;
   if (total > (int64_t)C.stage_cap) {
     const size_t cap = std::max<size_t>((size_t)total, C.stage_cap * 2);
-    MRAG_HIP(hipStreamSynchronize(s));
+    if (int rc = mrag::blocking_wait(s)) return rc;
     if (C.stage) (void)hipHostFree(C.stage);
     C.stage = nullptr;
     C.stage_cap = 0;
     MRAG_HIP(hipHostMalloc((void**)&C.stage, cap, hipHostMallocDefault));
     C.stage_cap = cap;
   }
-  MRAG_HIP(hipStreamSynchronize(s));  // the previous batch's copy out of the stage is done
+  if (int rc = mrag::blocking_wait(s)) return rc;  // the previous batch's copy out of the stage is done
   const int nth = (int)std::max<int64_t>(1, std::min<int64_t>({8, (int64_t)std::thread::hardware_concurrency(), (n + 3) / 4}));
   {
     std::vector<std::thread> th;
@@ -261,7 +261,7 @@ int mrag_png_unfilter(const uint8_t* const* raws, const int32_t* dims, int32_t n
   if (has[3]) launch(png_unfilter_kernel<3>);
   if (has[4]) launch(png_unfilter_kernel<4>);
   MRAG_CHECK_LAUNCH();
-  MRAG_HIP(hipStreamSynchronize(s));  // the descriptors live on this stack frame
+  if (int rc = mrag::blocking_wait(s)) return rc;  // the descriptors live on this stack frame
   return MRAG_OK;
 }
 
