@@ -19,6 +19,7 @@
 // Files K13 does not support (progressive, arithmetic, CMYK, 4:4:0, tiny chroma) are reported by
 // mrag_jpeg_probe and decoded on the host by the caller, as the reference decodes everything.
 #include <algorithm>
+#include <atomic>
 #include <cstring>
 #include <mutex>
 #include <thread>
@@ -186,7 +187,7 @@ Ctx g_ctx[64];
 
 extern "C" {
 
-int mrag_jpeg_probe(const uint8_t* data, int64_t size, int32_t* width, int32_t* height) {
+static int jpeg_probe_impl(const uint8_t* data, int64_t size, int32_t* width, int32_t* height) {
   if (!data || !width || !height || size < 0) return -mrag::fail(MRAG_ERR_ARG, "NULL argument");  // not 1
   Parsed P;
   if (!parse(data, size, P)) {
@@ -198,8 +199,8 @@ int mrag_jpeg_probe(const uint8_t* data, int64_t size, int32_t* width, int32_t* 
   return 1;
 }
 
-int mrag_jpeg_decode(const uint8_t* const* files, const int64_t* sizes, int32_t n, uint8_t* out,
-                     const int64_t* out_offsets, int32_t device, void* stream) {
+static int jpeg_decode_impl(const uint8_t* const* files, const int64_t* sizes, int32_t n, uint8_t* out,
+                            const int64_t* out_offsets, int32_t device, void* stream) {
   MRAG_REQUIRE(n >= 0, "negative batch");
   if (n == 0) return MRAG_OK;
   MRAG_REQUIRE(files && sizes && out && out_offsets, "NULL argument");
@@ -212,15 +213,24 @@ int mrag_jpeg_decode(const uint8_t* const* files, const int64_t* sizes, int32_t 
 
   // host threads over the files: parse, then (below) unstuff into the pinned stage
   const int nth = (int)std::max<int64_t>(1, std::min<int64_t>({8, (int64_t)std::thread::hardware_concurrency(), (n + 15) / 16}));
+  std::atomic<bool> thrown{false};  // an exception (allocation) on a host thread: reported, not std::terminate
   auto parallel = [&](auto fn) {
+    auto part = [&](int w) {
+      try {
+        for (int i = w; i < n; i += nth) fn(i);
+      } catch (...) {
+        thrown = true;
+      }
+    };
     std::vector<std::thread> th;
-    for (int w = 1; w < nth; ++w) th.emplace_back([&, w] { for (int i = w; i < n; i += nth) fn(i); });
-    for (int i = 0; i < n; i += nth) fn(i);
+    for (int w = 1; w < nth; ++w) th.emplace_back(part, w);
+    part(0);
     for (auto& x : th) x.join();
   };
   std::vector<Parsed> P((size_t)n);
   std::vector<char> ok((size_t)n, 0);
   parallel([&](int i) { ok[i] = parse(files[i], sizes[i], P[i]) ? 1 : 0; });
+  if (thrown) return mrag::fail(MRAG_ERR_OOM, "jpeg: host allocation failed while parsing");
   std::vector<Image> imgs((size_t)n);
   std::vector<ParSeg> segs;
   std::vector<int64_t> seg_src;  // raw segment start in its file
@@ -270,6 +280,7 @@ int mrag_jpeg_decode(const uint8_t* const* files, const int64_t* sizes, int32_t 
       segs[q].nbits = (uint32_t)(u * 8);
     }
   });
+  if (thrown) return mrag::fail(MRAG_ERR_OOM, "jpeg: host allocation failed while staging");
   if (int rc = ensure(C.ecs, (size_t)stage_bytes)) return rc;
   if (int rc = ensure(C.imgs, sizeof(Image) * (size_t)n)) return rc;
   if (int rc = ensure(C.segs, sizeof(ParSeg) * segs.size())) return rc;
@@ -291,6 +302,24 @@ int mrag_jpeg_decode(const uint8_t* const* files, const int64_t* sizes, int32_t 
   // the descriptors above live on this host stack frame: the copies must finish before return
   if (int rc = mrag::blocking_wait(s)) return rc;
   return MRAG_OK;
+}
+
+// the C ABI: no C++ exception crosses it (a failed host allocation is MRAG_ERR_OOM)
+int mrag_jpeg_probe(const uint8_t* data, int64_t size, int32_t* width, int32_t* height) {
+  try {
+    return jpeg_probe_impl(data, size, width, height);
+  } catch (...) {
+    return -mrag::fail(MRAG_ERR_OOM, "jpeg probe: host allocation failed");
+  }
+}
+
+int mrag_jpeg_decode(const uint8_t* const* files, const int64_t* sizes, int32_t n, uint8_t* out,
+                     const int64_t* out_offsets, int32_t device, void* stream) {
+  try {
+    return jpeg_decode_impl(files, sizes, n, out, out_offsets, device, stream);
+  } catch (...) {
+    return mrag::fail(MRAG_ERR_OOM, "jpeg decode: host allocation failed");
+  }
 }
 
 }  // extern "C"

@@ -178,7 +178,7 @@ Ctx g_ctx[64];
 
 extern "C" {
 
-int mrag_png_probe(const uint8_t* data, int64_t size, int32_t* width, int32_t* height, int64_t* raw_bytes) {
+static int png_probe_impl(const uint8_t* data, int64_t size, int32_t* width, int32_t* height, int64_t* raw_bytes) {
   if (!data || !width || !height || !raw_bytes || size < 0) return -mrag::fail(MRAG_ERR_ARG, "NULL argument");
   PngParsed P;
   if (!png_parse(data, size, P, true)) {
@@ -192,7 +192,7 @@ int mrag_png_probe(const uint8_t* data, int64_t size, int32_t* width, int32_t* h
   return 1;
 }
 
-int mrag_png_inflate(const uint8_t* data, int64_t size, uint8_t* raw, int64_t cap, int32_t* bpp) {
+static int png_inflate_impl(const uint8_t* data, int64_t size, uint8_t* raw, int64_t cap, int32_t* bpp) {
   if (!data || !raw || !bpp || size < 0) return -mrag::fail(MRAG_ERR_ARG, "NULL argument");
   PngParsed P;
   if (!png_parse(data, size, P, false)) return 0;
@@ -203,8 +203,8 @@ int mrag_png_inflate(const uint8_t* data, int64_t size, uint8_t* raw, int64_t ca
   return 1;
 }
 
-int mrag_png_unfilter(const uint8_t* const* raws, const int32_t* dims, int32_t n, uint8_t* out,
-                      const int64_t* out_offsets, int32_t device, void* stream) {
+static int png_unfilter_impl(const uint8_t* const* raws, const int32_t* dims, int32_t n, uint8_t* out,
+                             const int64_t* out_offsets, int32_t device, void* stream) {
   MRAG_REQUIRE(n >= 0, "negative batch");
   if (n == 0) return MRAG_OK;
   MRAG_REQUIRE(raws && dims && out && out_offsets, "NULL argument");
@@ -263,6 +263,32 @@ int mrag_png_unfilter(const uint8_t* const* raws, const int32_t* dims, int32_t n
   MRAG_CHECK_LAUNCH();
   if (int rc = mrag::blocking_wait(s)) return rc;  // the descriptors live on this stack frame
   return MRAG_OK;
+}
+
+// the C ABI: no C++ exception crosses it (a failed host allocation is MRAG_ERR_OOM)
+int mrag_png_probe(const uint8_t* data, int64_t size, int32_t* width, int32_t* height, int64_t* raw_bytes) {
+  try {
+    return png_probe_impl(data, size, width, height, raw_bytes);
+  } catch (...) {
+    return -mrag::fail(MRAG_ERR_OOM, "png probe: host allocation failed");
+  }
+}
+
+int mrag_png_inflate(const uint8_t* data, int64_t size, uint8_t* raw, int64_t cap, int32_t* bpp) {
+  try {
+    return png_inflate_impl(data, size, raw, cap, bpp);
+  } catch (...) {
+    return -mrag::fail(MRAG_ERR_OOM, "png inflate: host allocation failed");
+  }
+}
+
+int mrag_png_unfilter(const uint8_t* const* raws, const int32_t* dims, int32_t n, uint8_t* out,
+                      const int64_t* out_offsets, int32_t device, void* stream) {
+  try {
+    return png_unfilter_impl(raws, dims, n, out, out_offsets, device, stream);
+  } catch (...) {
+    return mrag::fail(MRAG_ERR_OOM, "png unfilter: host allocation failed");
+  }
 }
 
 }  // extern "C"
