@@ -509,8 +509,13 @@ def ingest_leg(n_images: int = 2048):
         t0 = time.perf_counter()
         prepared = [prepare_batch(paths[i:i + group]) for i in range(0, len(paths), group)]
         t_prep = time.perf_counter() - t0
-        k13_files = sum(1 for g in prepared for j, _ in g if j is not None and j[0] == "jpeg")
-        k14_files = sum(1 for g in prepared for j, _ in g if j is not None and j[0] == "png")
+        def _kinds(g):  # 1 JPEG (K13), 2 PNG (K14) per file of a prepared group, either host half
+            if hasattr(g, "kind"):
+                return g.kind.tolist()
+            return [0 if j is None else {"jpeg": 1, "png": 2}[j[0]] for j, _ in g]
+
+        k13_files = sum(k.count(1) for k in map(_kinds, prepared))
+        k14_files = sum(k.count(2) for k in map(_kinds, prepared))
         _sync()
         t0 = time.perf_counter()
         groups = [upload_decode(g) for g in prepared]

@@ -253,6 +253,22 @@ int mrag_png_inflate(const uint8_t* data, int64_t size, uint8_t* raw, int64_t ca
 int mrag_png_unfilter(const uint8_t* const* raws, const int32_t* dims, int32_t n, uint8_t* out,
                       const int64_t* out_offsets, int32_t device, void* stream);
 
+/* The host half of image ingest in one call (the per-file Image.open of the reference's
+ * embed_images_batch, app/ml/embeddings.py:82-89): mrag_files_prepare reads n files on `threads`
+ * host threads of its own and classifies each — kind 1: a JPEG K13 decodes, 2: a PNG K14
+ * reconstructs (inflated here), 0: anything else (decode it with Pillow), -1: unreadable (open it
+ * yourself to get the error); device_decode = 0 classifies every readable file as 0.
+ * mrag_files_info: kind / width / height per file (arrays of n). mrag_files_bytes: a file's bytes
+ * (valid until mrag_files_free). mrag_files_decode: K13 + K14 for the kind 1 / 2 files into
+ * device memory `out`, file i as H x W x 3 u8 RGB at out_offsets[i] (host array of n; entries of
+ * other kinds unused); synchronous on `stream`. */
+typedef struct mrag_files mrag_files;
+int mrag_files_prepare(const char* const* paths, int32_t n, int32_t threads, int32_t device_decode, mrag_files** out);
+int mrag_files_info(const mrag_files* files, int32_t* kind, int32_t* width, int32_t* height);
+int mrag_files_bytes(const mrag_files* files, int32_t i, const uint8_t** data, int64_t* size);
+int mrag_files_decode(const mrag_files* files, uint8_t* out, const int64_t* out_offsets, int32_t device, void* stream);
+int mrag_files_free(mrag_files* files);
+
 /* K3 building block: C[M][N] (op)= A[M][K] . W[N][K]^T + bias (device pointers;
  * A, W fp16 row-major; epilogue 0 f16 out, 1 f16 quick_gelu, 2 f16 gelu_erf,
  * 3 f32 C += , 4 f32 out). N % 128 == 0, K % 64 == 0; bias and C 16-byte aligned. */

@@ -184,11 +184,65 @@ def _prepare_one(x):
         return None, np.asarray(im.convert("RGB"), dtype=np.uint8)
 
 
+class NativePrepared:
+    """A group's host half done by the library (``mrag_files_prepare``: file reads, probes and the
+    PNGs' inflate on its own threads, no interpreter lock between files): the handle owning the
+    bytes K13 / K14 decode from, each file's kind and size, and Pillow arrays for the files the GPU
+    decoders do not take (kind 0). Unreadable files raise here, as Image.open would."""
+
+    def __init__(self, paths: Sequence[Union[str, Path]]):
+        from app import _native
+
+        lib = _native.load()
+        n = len(paths)
+        names = (ctypes.c_char_p * n)(*[os.fsencode(os.fspath(p)) for p in paths])
+        h = ctypes.c_void_p()
+        dev = 0 if os.environ.get("MRAG_HOST_DECODE") == "1" else 1
+        _native.call("mrag_files_prepare", ctypes.cast(names, ctypes.c_void_p), n, decode_workers(), dev,
+                     ctypes.byref(h))
+        self._lib, self.handle = lib, h
+        kind, w, hh = (np.zeros(n, np.int32) for _ in range(3))
+        _native.call("mrag_files_info", h, kind.ctypes.data, w.ctypes.data, hh.ctypes.data)
+        self.kind = kind
+        self.dims = np.stack([hh, w], axis=1).astype(np.int64)
+        self.host: dict = {}
+        for i in np.nonzero(kind <= 0)[0]:
+            i = int(i)
+            if kind[i] < 0:  # the reference's error for this path (or, if it reads now, its decode)
+                with open(paths[i], "rb") as f:
+                    b = f.read()
+            else:
+                ptr, size = ctypes.c_void_p(), ctypes.c_int64()
+                _native.call("mrag_files_bytes", h, i, ctypes.byref(ptr), ctypes.byref(size))
+                b = ctypes.string_at(ptr.value, size.value) if size.value else b""
+            with Image.open(io.BytesIO(b)) as im:
+                a = np.asarray(im.convert("RGB"), dtype=np.uint8)
+            self.host[i] = a
+            self.dims[i] = a.shape[:2]
+
+    def __len__(self):
+        return len(self.kind)
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h is not None and h.value:
+            self._lib.mrag_files_free(h)
+            self.handle = None
+
+
+_NATIVE_FILES = True  # path lists through mrag_files_prepare (False: _prepare_one per file on the pool)
+
+
 def prepare_batch(items: Sequence[Union[str, Path, Image.Image]]) -> list:
-    """The host half of ``load_batch_device`` on the process-wide pool: file bytes of the JPEGs the
-    GPU decodes, inflated scanlines of the PNGs it reconstructs, Pillow arrays of everything else (embed_images_batch runs it for the next batch
-    while the GPU works on the current one)."""
-    return list(_pool().map(_prepare_one, items)) if len(items) else []
+    """The host half of ``load_batch_device``: for a list of file paths one library call
+    (``NativePrepared``); otherwise per item on the process-wide pool — file bytes of the JPEGs the
+    GPU decodes, inflated scanlines of the PNGs it reconstructs, Pillow arrays of everything else
+    (embed_images_batch runs it for the next batch while the GPU works on the current one)."""
+    if len(items) == 0:
+        return []
+    if _NATIVE_FILES and all(isinstance(x, (str, Path)) for x in items):
+        return NativePrepared(list(items))
+    return list(_pool().map(_prepare_one, items))
 
 
 class DeviceImages:
@@ -212,6 +266,31 @@ def upload_decode(prepared: list, device: int = 0) -> DeviceImages:
 
     n = len(prepared)
     dev = torch.device("cuda", device)
+    if isinstance(prepared, NativePrepared):
+        dims = prepared.dims
+        sizes = dims[:, 0] * dims[:, 1] * 3
+        host = sorted(prepared.host)
+        gpu = [i for i in range(n) if prepared.kind[i] > 0]
+        offsets = np.zeros(n, dtype=np.int64)  # host-decoded images first (one copy), then K13's / K14's
+        pos = 0
+        for i in host + gpu:
+            offsets[i] = pos
+            pos += int(sizes[i])
+        pix = torch.empty(max(pos, 1), dtype=torch.uint8, device=dev)
+        with torch.cuda.device(dev):
+            stream = torch.cuda.current_stream(dev).cuda_stream
+            if host:
+                nh = int(sum(int(sizes[i]) for i in host))
+                staging = torch.empty(nh, dtype=torch.uint8, pin_memory=True)
+                sv = staging.numpy()
+                for i in host:
+                    sv[offsets[i]:offsets[i] + sizes[i]] = prepared.host[i].reshape(-1)
+                pix[:nh].copy_(staging, non_blocking=True)
+            if gpu:
+                _native.call("mrag_files_decode", prepared.handle, pix.data_ptr(), offsets.ctypes.data, device, stream)
+            else:
+                torch.cuda.current_stream(dev).synchronize()  # a lone copy is complete on return too
+        return DeviceImages(pix, offsets, dims)
     for j, a in prepared:
         if a is not None and (a.ndim != 3 or a.shape[2] != 3):
             raise ValueError(f"expected HxWx3 u8 images, got shape {a.shape}")

@@ -25,8 +25,10 @@ from app.settings import settings
 
 _TEXT_MODEL: Optional[Any] = None
 _DECODE_GROUP_BATCHES = 1  # encoder batches per K13 decode launch (profiles/r5s18_ingest_group_ab.jsonl)
-_PREP_PER_FILE = True  # host half per file, two groups ahead (False: one prepare_batch per group;
-# profiles/r5s35_prep_ab.jsonl: 11.2k vs 10.3k img/s, three interleaved pairs)
+_PREP_PER_FILE = False  # False: one prepare_batch per group, two groups ahead — for path lists one
+# library call (preprocess.NativePrepared; profiles/r5s37_native_ab.jsonl: 16.6-18.2k img/s vs
+# 11.4-12.8k per file, three interleaved rounds). True: the host half per file on the decode pool
+# (the better of the two Python host halves: profiles/r5s35_prep_ab.jsonl, 11.2k vs 10.3k img/s)
 _CLIP_MODEL: Optional[Any] = None
 _CLIP_PROCESSOR: Optional[Any] = None
 

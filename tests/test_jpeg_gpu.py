@@ -121,3 +121,27 @@ def test_damaged_files_as_pillow(cuda, tmp_path):
     assert refused
     with pytest.raises(OSError):
         load_batch_device(ok[:3] + refused[:1])
+
+
+def test_embed_images_batch_group_host_half_equals_per_file(cuda, tmp_path):
+    """embed_images_batch with the host half as one library call per group (_PREP_PER_FILE False:
+    processor.decode -> NativePrepared) equals the per-file submission bit for bit."""
+    from PIL import Image
+
+    from app.ml import embeddings as emb
+
+    paths = []
+    for i in range(300):
+        a = photo(110 + i % 7, 150, 3000 + i)
+        p = tmp_path / (f"g{i}.png" if i % 4 == 3 else f"g{i}.jpg")
+        Image.fromarray(a).save(p, **({} if i % 4 == 3 else {"quality": 85}))
+        paths.append(str(p))
+    keep = emb._PREP_PER_FILE
+    try:
+        emb._PREP_PER_FILE = True
+        per_file = emb.embed_images_batch(paths)
+        emb._PREP_PER_FILE = False
+        group = emb.embed_images_batch(paths)
+    finally:
+        emb._PREP_PER_FILE = keep
+    np.testing.assert_array_equal(group, per_file)

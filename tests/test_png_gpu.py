@@ -95,3 +95,51 @@ def test_load_batch_device_png_mix_equals_host(cuda, tmp_path):
         np.testing.assert_array_equal(load_batch_device(items).cpu().numpy(), ref)
     finally:
         del os.environ["MRAG_HOST_DECODE"]
+
+
+def test_native_files_equal_per_file_path(cuda, tmp_path):
+    """The group host half in one library call (NativePrepared: mrag_files_prepare, then
+    mrag_files_decode) gives the per-file path's device pixels byte for byte over JPEGs, PNGs K14
+    takes and files both leave to Pillow; a missing file raises FileNotFoundError in both."""
+    import torch
+
+    from _jpeg_cases import photo
+    from PIL import Image
+
+    from app.encoders import preprocess as pp
+
+    items = []
+    sup = [c for c in supported_cases() if c[0].startswith(("photo480x640", "noise201x300", "filters300x201"))]
+    left = [c for c in unsupported_cases() if c[0] != "bad_crc"]
+    for i, (name, b) in enumerate(sup + left):
+        p = tmp_path / f"{i}_{name}.png"
+        p.write_bytes(b)
+        items.append(str(p))
+    for i in range(3):
+        p = tmp_path / f"j{i}.jpg"
+        Image.fromarray(photo(300 + 40 * i, 400, 50 + i)).save(p, quality=90, progressive=(i == 2))
+        items.append(str(p))
+
+    def dev_pixels(flag):
+        pp._NATIVE_FILES = flag
+        try:
+            prep = pp.prepare_batch(items)
+            assert isinstance(prep, pp.NativePrepared) == flag
+            d = pp.upload_decode(prep, device=0)
+            torch.cuda.synchronize()
+            return [d.pix[int(o):int(o) + int(h * w * 3)].cpu().numpy().reshape(h, w, 3)
+                    for o, (h, w) in zip(d.offsets, d.dims)]
+        finally:
+            pp._NATIVE_FILES = True
+
+    nat, per = dev_pixels(True), dev_pixels(False)
+    for p, a, b in zip(items, nat, per):
+        np.testing.assert_array_equal(a, b, err_msg=p)
+    assert pp.NativePrepared(items).kind.tolist().count(0) == len(left) + 1  # + the progressive JPEG
+    for flag in (True, False):
+        pp._NATIVE_FILES = flag
+        try:
+            with pytest.raises(FileNotFoundError):
+                pp.load_batch_device(items[:2] + [str(tmp_path / "missing.png")])
+        finally:
+            pp._NATIVE_FILES = True
