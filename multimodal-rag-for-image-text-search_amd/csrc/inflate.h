@@ -1,6 +1,8 @@
 // inflate.h — host-side DEFLATE / zlib decoder for K14's PNG path (RFC 1950 / RFC 1951), written
 // for throughput: a 64-bit bit buffer refilled eight bytes at a time, two-level Huffman tables
-// (a direct primary lookup, subtables for the longer codes), match copies in 8-byte words.
+// (a direct primary lookup, subtables for the longer codes) whose primary entries hold two
+// literals when both codes fit in its bits (PNG scanlines after filtering are mostly literals with
+// short codes: one lookup then writes two bytes), match copies in 8-byte words.
 // It applies zlib's validity rules (inftrees.c: over-subscribed code sets and incomplete ones are
 // errors, except a single code of length 1 for literal/length and distance codes; inflate.c:
 // header check, no preset dictionary, HLIT <= 286, HDIST <= 30, a repeat with no previous length,
@@ -25,10 +27,12 @@ namespace mrag_png {
 
 namespace infl {
 
-constexpr int LBITS = 10, DBITS = 8;  // primary table bits (literal/length, distance)
-// entry: bits 0-4 code length to consume (primary or whole code), bit 5: subtable pointer,
-// bit 6: invalid, bits 8-15: subtable bits, bits 16-31: symbol or subtable offset
-constexpr uint32_t SUB = 1u << 5, BAD = 1u << 6, LIT = 1u << 7;  // LIT: a literal (literal/length table)
+constexpr int LBITS = 11, DBITS = 8;  // primary table bits (literal/length, distance)
+// entry: bits 0-4 bits to consume (primary or whole code; a literal entry: all its literals),
+// bit 5: subtable pointer, bit 6: invalid, bits 16-31: symbol or subtable offset.
+// SUB entries: bits 8-15 subtable bits. LIT entries (literal/length table, symbol < 256): bits 8-12
+// the first literal's code length, bit 13 PAIR (bits 16-23 the first literal, 24-31 the second)
+constexpr uint32_t SUB = 1u << 5, BAD = 1u << 6, LIT = 1u << 7, PAIR = 1u << 13;
 
 struct Table {
   uint32_t e[(1 << LBITS) + 32 * 1024];  // worst case: every primary slot owns a subtable
@@ -96,15 +100,27 @@ inline bool build(Table& t, const uint8_t* lens, int n, int kind, int pbits) {
     if (!len) continue;
     const uint32_t r = rev((uint32_t)code_of[s], len);
     if (len <= pbits) {
-      const uint32_t lit = kind == 1 && s < 256 ? LIT : 0u;
+      const uint32_t lit = kind == 1 && s < 256 ? LIT | (uint32_t)len << 8 : 0u;
       for (uint32_t i = r; i < (uint32_t)psize; i += 1u << len) t.e[i] = (uint32_t)len | lit | ((uint32_t)s << 16);
     } else {
       const int p = (int)(r & (uint32_t)(psize - 1));
       const uint32_t base = t.e[p] >> 16;
       const int sb = (int)((t.e[p] >> 8) & 0xFF), rem = len - pbits;
-      const uint32_t lit = kind == 1 && s < 256 ? LIT : 0u;
+      const uint32_t lit = kind == 1 && s < 256 ? LIT | (uint32_t)rem << 8 : 0u;
       for (uint32_t i = r >> pbits; i < (1u << sb); i += 1u << rem)
         t.e[base + i] = (uint32_t)rem | lit | ((uint32_t)s << 16);
+    }
+  }
+  if (kind == 1) {  // literal pairs: index i's first code a literal of l1 bits, the next in the
+    // remaining pbits - l1 bits (its entry at i >> l1 of the single-symbol table) a literal too
+    uint32_t one[1 << LBITS];
+    std::memcpy(one, t.e, sizeof(uint32_t) * (size_t)psize);
+    for (int i = 0; i < psize; ++i) {
+      const uint32_t e1 = one[i];
+      if (!(e1 & LIT)) continue;
+      const uint32_t l1 = e1 & 31, e2 = one[i >> l1];
+      if ((e2 & LIT) && l1 + (e2 & 31) <= (uint32_t)pbits)
+        t.e[i] = (l1 + (e2 & 31)) | LIT | PAIR | l1 << 8 | (e1 >> 16 & 0xFFu) << 16 | (e2 >> 16 & 0xFFu) << 24;
     }
   }
   return true;
@@ -170,6 +186,10 @@ inline int decode(Bits& b, const Table& t) {
     e = t.e[(e >> 16) + b.peek(sb)];
   }
   if (e & BAD) return -1;
+  if (e & LIT) {  // the first literal of the entry
+    b.drop((int)(e >> 8 & 31));
+    return (int)(e >> 16 & 0xFF);
+  }
   b.drop((int)(e & 31));
   return (int)(e >> 16);
 }
@@ -272,21 +292,26 @@ inline bool fast_inflate(const uint8_t* in, size_t in_len, uint8_t* out, size_t 
     // the block's symbols
     while (true) {
       // hot loop: >= 16 input bytes and >= 274 output bytes left, so no end checks; up to three
-      // literals per refill (>= 56 bits: 3 x 15); the general symbol after them as below
+      // primary literal entries (one or two literals, <= LBITS bits each) per refill (>= 56 bits:
+      // 3 x 11 + a length code with its extra bits, 20), each stored as two bytes; the general
+      // symbol after them as below
       while (b.end - b.p >= 16 && oend - op >= 274) {
         b.refill_fast();
         uint32_t e = lt.e[b.peek(LBITS)];
         if (e & LIT) {
-          b.drop((int)(e & 31));
-          *op++ = (uint8_t)(e >> 16);
+          auto put = [&](uint32_t x) {
+            b.drop((int)(x & 31));
+            const uint16_t two = (uint16_t)(x >> 16);
+            std::memcpy(op, &two, 2);
+            op += 1 + (x >> 13 & 1);
+          };
+          put(e);
           e = lt.e[b.peek(LBITS)];
           if (e & LIT) {
-            b.drop((int)(e & 31));
-            *op++ = (uint8_t)(e >> 16);
+            put(e);
             e = lt.e[b.peek(LBITS)];
             if (e & LIT) {
-              b.drop((int)(e & 31));
-              *op++ = (uint8_t)(e >> 16);
+              put(e);
               continue;
             }
           }

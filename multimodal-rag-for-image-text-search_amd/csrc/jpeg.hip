@@ -7,7 +7,7 @@
 // to the device in one copy, and three kernels run:
 //   K13a jpeg_huff_par_kernel  one workgroup per entropy-coded segment (a whole image, or one
 //                           restart interval), one chunk of the segment's bits per lane (up to
-//                           256): self-synchronising parallel Huffman decode (jpeg_core.h,
+//                           1024): self-synchronising parallel Huffman decode (jpeg_core.h,
 //                           par_run) into zeroed int16 coefficient blocks, the same tokens and
 //                           values as the sequential decoder (round 5 first shipped that one, one
 //                           single-lane workgroup per segment: 70-78 ms per launch, the largest

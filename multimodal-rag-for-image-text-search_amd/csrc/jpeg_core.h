@@ -239,8 +239,12 @@ struct PCheck {
   int32_t n[4];  // completed blocks, DC-difference sums of components 0..2 since the entry
 };
 constexpr int PAR_NCP = 4;         // checkpoints per chunk
-constexpr int PAR_LANES = 256;     // lanes (chunks) per segment at most
-constexpr int PAR_MIN_BITS = 4096; // shortest chunk
+#ifndef MRAG_PAR_LANES  // (overridable for A/B builds only; 256 x 4096: K13a 2.87 ms per ingest
+#define MRAG_PAR_LANES 1024  // group, 512 x 2048: 1.94, 1024 x 1024: 1.67 — profiles/r5s41_*)
+#define MRAG_PAR_MIN_BITS 1024
+#endif
+constexpr int PAR_LANES = MRAG_PAR_LANES;        // lanes (chunks) per segment at most
+constexpr int PAR_MIN_BITS = MRAG_PAR_MIN_BITS;  // shortest chunk
 
 // Per-image tables for the parallel decoder: the four Huffman tables and, per block of the MCU,
 // its component and table ids.

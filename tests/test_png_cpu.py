@@ -137,6 +137,12 @@ def test_fast_inflate_equals_zlib(host_check):
         else:
             d = np.cumsum(rng.integers(-2, 3, n)).astype(np.uint8).tobytes()
         datas.append(d)
+    for i in range(4):  # skewed small alphabets, like filtered scanlines: short literal codes, so the
+        # decoder's two-literal table entries; outputs cut at every offset near the end below
+        n = int(rng.integers(2000, 60000))
+        g = np.minimum(rng.geometric(0.25 + 0.15 * i, n), 60).astype(np.int64)
+        d = np.where(rng.random(n) < 0.5, g, 256 - g).astype(np.uint8).tobytes()
+        datas.append(d)
     strategies = [zlib.Z_DEFAULT_STRATEGY, zlib.Z_FILTERED, zlib.Z_HUFFMAN_ONLY, zlib.Z_RLE, zlib.Z_FIXED]
     for d in datas:
         for lvl in (0, 1, 6, 9):
@@ -145,6 +151,12 @@ def test_fast_inflate_equals_zlib(host_check):
                 s = c.compress(d) + c.flush()
                 for n in (len(d), max(1, len(d) // 2)):
                     assert fast(s, n) == ref(s, n), (len(d), lvl, st, n)
+    for d in datas[-4:]:
+        for st in (zlib.Z_DEFAULT_STRATEGY, zlib.Z_HUFFMAN_ONLY):
+            c = zlib.compressobj(6, zlib.DEFLATED, 15, 8, st)
+            s = c.compress(d) + c.flush()
+            for n in list(range(max(1, len(d) - 300), len(d) + 1)) + list(range(1, 300)):
+                assert fast(s, n) == ref(s, n), (len(d), st, n)
     agree = 0
     for t in range(1500):
         d = datas[t % len(datas)]
