@@ -27,6 +27,7 @@
 
 #include "common.h"
 #include "jpeg_parse.h"
+#include "staged.h"
 
 using namespace mrag_jpeg;
 
@@ -199,13 +200,17 @@ static int jpeg_probe_impl(const uint8_t* data, int64_t size, int32_t* width, in
   return 1;
 }
 
+// st == nullptr: parse the files and unstuff their segments here; otherwise the caller's staged
+// parse and unstuffed bytes (staged.h; files / sizes unused)
 static int jpeg_decode_impl(const uint8_t* const* files, const int64_t* sizes, int32_t n, uint8_t* out,
-                            const int64_t* out_offsets, int32_t device, void* stream) {
+                            const int64_t* out_offsets, int32_t device, void* stream,
+                            const mrag_stage::JpegStaged* st) {
   MRAG_REQUIRE(n >= 0, "negative batch");
   if (n == 0) return MRAG_OK;
-  MRAG_REQUIRE(files && sizes && out && out_offsets, "NULL argument");
+  MRAG_REQUIRE((st ? (st->P && st->stage && st->nbits) : (files && sizes)) && out && out_offsets, "NULL argument");
   MRAG_REQUIRE(device >= 0 && device < 64, "bad device %d", device);
-  for (int i = 0; i < n; ++i) MRAG_REQUIRE(files[i] != nullptr && sizes[i] >= 0, "bad file %d", i);
+  if (!st)
+    for (int i = 0; i < n; ++i) MRAG_REQUIRE(files[i] != nullptr && sizes[i] >= 0, "bad file %d", i);
   mrag::DeviceGuard g(device);
   Ctx& C = g_ctx[device];
   std::lock_guard<std::mutex> lk(C.mu);
@@ -227,23 +232,30 @@ static int jpeg_decode_impl(const uint8_t* const* files, const int64_t* sizes, i
     part(0);
     for (auto& x : th) x.join();
   };
-  std::vector<Parsed> P((size_t)n);
-  std::vector<char> ok((size_t)n, 0);
-  parallel([&](int i) { ok[i] = parse(files[i], sizes[i], P[i]) ? 1 : 0; });
-  if (thrown) return mrag::fail(MRAG_ERR_OOM, "jpeg: host allocation failed while parsing");
+  std::vector<Parsed> Pv;
+  std::vector<const Parsed*> P((size_t)n);
+  std::vector<char> ok((size_t)n, 1);
+  if (st) {
+    for (int i = 0; i < n; ++i) P[i] = st->P[i];
+  } else {
+    Pv.resize((size_t)n);
+    parallel([&](int i) { ok[i] = parse(files[i], sizes[i], Pv[i]) ? 1 : 0; });
+    if (thrown) return mrag::fail(MRAG_ERR_OOM, "jpeg: host allocation failed while parsing");
+    for (int i = 0; i < n; ++i) P[i] = &Pv[i];
+  }
   std::vector<Image> imgs((size_t)n);
   std::vector<ParSeg> segs;
   std::vector<int64_t> seg_src;  // raw segment start in its file
   std::vector<int64_t> seg_len;
   int64_t stage_bytes = 0, blocks = 0, planes = 0, max_blocks = 0, max_quads = 0;
   for (int i = 0; i < n; ++i) {
-    if (!ok[i]) return mrag::fail(MRAG_ERR_ARG, "jpeg %d unsupported: %s", i, P[i].why.c_str());
-    Image& im = imgs[i] = P[i].img;
+    if (!ok[i]) return mrag::fail(MRAG_ERR_ARG, "jpeg %d unsupported: %s", i, P[i]->why.c_str());
+    Image& im = imgs[i] = P[i]->img;
     im.seg0 = (int32_t)segs.size();
     im.coef_off = blocks;
     im.plane_off = planes;
     im.rgb_off = out_offsets[i];
-    for (const Segment& sg : P[i].segs) {
+    for (const Segment& sg : P[i]->segs) {
       MRAG_REQUIRE(sg.len < (1ll << 28), "jpeg %d: entropy-coded segment of %lld bytes", i, (long long)sg.len);
       ParSeg ps;
       ps.uoff = stage_bytes;
@@ -254,14 +266,20 @@ static int jpeg_decode_impl(const uint8_t* const* files, const int64_t* sizes, i
       segs.push_back(ps);
       seg_src.push_back(sg.off);
       seg_len.push_back(sg.len);
-      stage_bytes += (sg.len + 15) / 16 * 16 + 16;  // unstuffed <= raw; zero tail to 16 bytes
+      stage_bytes += mrag_stage::jpeg_seg_stage_bytes(sg.len);  // unstuffed <= raw; zero tail to 16 bytes
     }
-    blocks += P[i].coef_blocks;
-    planes += P[i].plane_bytes;
-    max_blocks = std::max(max_blocks, P[i].coef_blocks);
+    blocks += P[i]->coef_blocks;
+    planes += P[i]->plane_bytes;
+    max_blocks = std::max(max_blocks, P[i]->coef_blocks);
     max_quads = std::max(max_quads, (int64_t)(im.width + 3) / 4 * im.height);
   }
-  if (stage_bytes > (int64_t)C.stage_cap) {
+  const uint8_t* src = C.stage;
+  if (st) {
+    MRAG_REQUIRE(st->bytes == stage_bytes, "jpeg: staged %lld bytes, the layout needs %lld", (long long)st->bytes,
+                 (long long)stage_bytes);
+    for (size_t q = 0; q < segs.size(); ++q) segs[q].nbits = st->nbits[q];
+    src = st->stage;
+  } else if (stage_bytes > (int64_t)C.stage_cap) {
     const size_t cap = std::max<size_t>((size_t)stage_bytes, C.stage_cap * 2);
     if (int rc = mrag::blocking_wait(s)) return rc;  // a previous batch's copy may still read the old buffer
     if (C.stage) (void)hipHostFree(C.stage);
@@ -270,23 +288,26 @@ static int jpeg_decode_impl(const uint8_t* const* files, const int64_t* sizes, i
     MRAG_HIP(hipHostMalloc((void**)&C.stage, cap, hipHostMallocDefault));
     C.stage_cap = cap;
   }
-  // the previous batch's copy out of the staging buffer must be done before it is rewritten
-  if (int rc = mrag::blocking_wait(s)) return rc;
-  parallel([&](int i) {
-    for (int q = imgs[i].seg0, e = imgs[i].seg0 + (int)P[i].segs.size(); q < e; ++q) {
-      uint8_t* dst = C.stage + segs[q].uoff;
-      const int64_t u = unstuff(files[i] + seg_src[q], seg_len[q], dst);
-      std::memset(dst + u, 0, (size_t)((u + 15) / 16 * 16 - u));
-      segs[q].nbits = (uint32_t)(u * 8);
-    }
-  });
-  if (thrown) return mrag::fail(MRAG_ERR_OOM, "jpeg: host allocation failed while staging");
+  if (!st) {
+    // the previous batch's copy out of the staging buffer must be done before it is rewritten
+    if (int rc = mrag::blocking_wait(s)) return rc;
+    src = C.stage;
+    parallel([&](int i) {
+      for (int q = imgs[i].seg0, e = imgs[i].seg0 + (int)P[i]->segs.size(); q < e; ++q) {
+        uint8_t* dst = C.stage + segs[q].uoff;
+        const int64_t u = unstuff(files[i] + seg_src[q], seg_len[q], dst);
+        std::memset(dst + u, 0, (size_t)((u + 15) / 16 * 16 - u));
+        segs[q].nbits = (uint32_t)(u * 8);
+      }
+    });
+    if (thrown) return mrag::fail(MRAG_ERR_OOM, "jpeg: host allocation failed while staging");
+  }
   if (int rc = ensure(C.ecs, (size_t)stage_bytes)) return rc;
   if (int rc = ensure(C.imgs, sizeof(Image) * (size_t)n)) return rc;
   if (int rc = ensure(C.segs, sizeof(ParSeg) * segs.size())) return rc;
   if (int rc = ensure(C.coef, (size_t)blocks * 128)) return rc;
   if (int rc = ensure(C.planes, (size_t)planes)) return rc;
-  MRAG_HIP(hipMemcpyAsync(C.ecs.p, C.stage, (size_t)stage_bytes, hipMemcpyHostToDevice, s));
+  MRAG_HIP(hipMemcpyAsync(C.ecs.p, src, (size_t)stage_bytes, hipMemcpyHostToDevice, s));
   MRAG_HIP(hipMemcpyAsync(C.imgs.p, imgs.data(), sizeof(Image) * (size_t)n, hipMemcpyHostToDevice, s));
   MRAG_HIP(hipMemcpyAsync(C.segs.p, segs.data(), sizeof(ParSeg) * segs.size(), hipMemcpyHostToDevice, s));
   MRAG_HIP(hipMemsetAsync(C.coef.p, 0, (size_t)blocks * 128, s));
@@ -316,10 +337,19 @@ int mrag_jpeg_probe(const uint8_t* data, int64_t size, int32_t* width, int32_t* 
 int mrag_jpeg_decode(const uint8_t* const* files, const int64_t* sizes, int32_t n, uint8_t* out,
                      const int64_t* out_offsets, int32_t device, void* stream) {
   try {
-    return jpeg_decode_impl(files, sizes, n, out, out_offsets, device, stream);
+    return jpeg_decode_impl(files, sizes, n, out, out_offsets, device, stream, nullptr);
   } catch (...) {
     return mrag::fail(MRAG_ERR_OOM, "jpeg decode: host allocation failed");
   }
 }
 
 }  // extern "C"
+
+int mrag_stage::jpeg_decode_staged(const JpegStaged& st, int32_t n, uint8_t* out, const int64_t* out_offsets,
+                                   int32_t device, void* stream) {
+  try {
+    return jpeg_decode_impl(nullptr, nullptr, n, out, out_offsets, device, stream, &st);
+  } catch (...) {
+    return mrag::fail(MRAG_ERR_OOM, "jpeg decode: host allocation failed");
+  }
+}

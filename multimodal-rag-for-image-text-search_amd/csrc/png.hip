@@ -27,6 +27,7 @@
 
 #include "common.h"
 #include "png_parse.h"
+#include "staged.h"
 
 using namespace mrag_png;
 
@@ -203,27 +204,34 @@ static int png_inflate_impl(const uint8_t* data, int64_t size, uint8_t* raw, int
   return 1;
 }
 
+// staged == nullptr: raws[i] anywhere in host memory, copied here into the pinned stage; otherwise
+// image i's scanlines at staged + raw_off[i], inside staged[0 .. staged_bytes) (staged.h)
 static int png_unfilter_impl(const uint8_t* const* raws, const int32_t* dims, int32_t n, uint8_t* out,
-                             const int64_t* out_offsets, int32_t device, void* stream) {
+                             const int64_t* out_offsets, int32_t device, void* stream, const uint8_t* staged,
+                             int64_t staged_bytes, const int64_t* raw_off) {
   MRAG_REQUIRE(n >= 0, "negative batch");
   if (n == 0) return MRAG_OK;
-  MRAG_REQUIRE(raws && dims && out && out_offsets, "NULL argument");
+  MRAG_REQUIRE((staged ? raw_off != nullptr : raws != nullptr) && dims && out && out_offsets, "NULL argument");
   MRAG_REQUIRE(device >= 0 && device < 64, "bad device %d", device);
   std::vector<PngImg> imgs((size_t)n);
   int64_t total = 0;
   for (int i = 0; i < n; ++i) {
     const int w = dims[3 * i], h = dims[3 * i + 1], bpp = dims[3 * i + 2];
-    MRAG_REQUIRE(raws[i] != nullptr, "NULL image %d", i);
+    MRAG_REQUIRE(staged || raws[i] != nullptr, "NULL image %d", i);
     MRAG_REQUIRE(w >= 1 && w <= PNG_MAXW && h >= 1 && h <= 65535 && bpp >= 1 && bpp <= 4,
                  "png %d: %d x %d, %d bytes per pixel unsupported", i, w, h, bpp);
-    imgs[i] = PngImg{total, out_offsets[i], w, h, bpp, 0};
-    total += (int64_t)h * (1 + (int64_t)w * bpp);
+    const int64_t bytes = (int64_t)h * (1 + (int64_t)w * bpp);
+    if (staged)
+      MRAG_REQUIRE(raw_off[i] >= 0 && raw_off[i] + bytes <= staged_bytes, "png %d: scanlines outside the stage", i);
+    imgs[i] = PngImg{staged ? raw_off[i] : total, out_offsets[i], w, h, bpp, 0};
+    total += bytes;
   }
+  if (staged) total = staged_bytes;
   mrag::DeviceGuard g(device);
   Ctx& C = g_ctx[device];
   std::lock_guard<std::mutex> lk(C.mu);
   hipStream_t s = (hipStream_t)stream;
-  if (total > (int64_t)C.stage_cap) {
+  if (!staged && total > (int64_t)C.stage_cap) {
     const size_t cap = std::max<size_t>((size_t)total, C.stage_cap * 2);
     if (int rc = mrag::blocking_wait(s)) return rc;
     if (C.stage) (void)hipHostFree(C.stage);
@@ -232,9 +240,10 @@ static int png_unfilter_impl(const uint8_t* const* raws, const int32_t* dims, in
     MRAG_HIP(hipHostMalloc((void**)&C.stage, cap, hipHostMallocDefault));
     C.stage_cap = cap;
   }
-  if (int rc = mrag::blocking_wait(s)) return rc;  // the previous batch's copy out of the stage is done
-  const int nth = (int)std::max<int64_t>(1, std::min<int64_t>({8, (int64_t)std::thread::hardware_concurrency(), (n + 3) / 4}));
-  {
+  if (!staged) {
+    if (int rc = mrag::blocking_wait(s)) return rc;  // the previous batch's copy out of the stage is done
+    const int nth =
+        (int)std::max<int64_t>(1, std::min<int64_t>({8, (int64_t)std::thread::hardware_concurrency(), (n + 3) / 4}));
     std::vector<std::thread> th;
     auto copy = [&](int w0) {
       for (int i = w0; i < n; i += nth)
@@ -247,7 +256,7 @@ static int png_unfilter_impl(const uint8_t* const* raws, const int32_t* dims, in
   }
   if (int rc = ensure(C.raw, (size_t)total)) return rc;
   if (int rc = ensure(C.imgs, sizeof(PngImg) * (size_t)n)) return rc;
-  MRAG_HIP(hipMemcpyAsync(C.raw.p, C.stage, (size_t)total, hipMemcpyHostToDevice, s));
+  MRAG_HIP(hipMemcpyAsync(C.raw.p, staged ? staged : C.stage, (size_t)total, hipMemcpyHostToDevice, s));
   MRAG_HIP(hipMemcpyAsync(C.imgs.p, imgs.data(), sizeof(PngImg) * (size_t)n, hipMemcpyHostToDevice, s));
   // one launch per pixel size present (a workgroup of another size returns at once)
   bool has[5] = {false, false, false, false, false};
@@ -285,10 +294,19 @@ int mrag_png_inflate(const uint8_t* data, int64_t size, uint8_t* raw, int64_t ca
 int mrag_png_unfilter(const uint8_t* const* raws, const int32_t* dims, int32_t n, uint8_t* out,
                       const int64_t* out_offsets, int32_t device, void* stream) {
   try {
-    return png_unfilter_impl(raws, dims, n, out, out_offsets, device, stream);
+    return png_unfilter_impl(raws, dims, n, out, out_offsets, device, stream, nullptr, 0, nullptr);
   } catch (...) {
     return mrag::fail(MRAG_ERR_OOM, "png unfilter: host allocation failed");
   }
 }
 
 }  // extern "C"
+
+int mrag_stage::png_unfilter_staged(const uint8_t* stage, int64_t bytes, const int64_t* raw_off, const int32_t* dims,
+                                    int32_t n, uint8_t* out, const int64_t* out_offsets, int32_t device, void* stream) {
+  try {
+    return png_unfilter_impl(nullptr, dims, n, out, out_offsets, device, stream, stage, bytes, raw_off);
+  } catch (...) {
+    return mrag::fail(MRAG_ERR_OOM, "png unfilter: host allocation failed");
+  }
+}
