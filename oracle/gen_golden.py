@@ -234,7 +234,7 @@ def main():
     with open(os.path.join(OUT, "golden_format.json"), "w") as f:
         json.dump({"rows": rows, "expected": RefStore._format_results(rows)}, f, indent=1)
 
-    # ---------------- kNN (oracle, pinned against sklearn in tests/test_oracle_knn.py)
+    # ---------------- kNN (oracle, pinned against sklearn in tests/test_oracle_pinning.py)
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from _data import clustered_corpus, labels_for, sha, unit_rows
 
