@@ -537,13 +537,14 @@ def ingest_leg(n_images: int = 2048):
         decode_batch(paths)  # every file with Pillow on the pool: the host decode K13 replaces
         t_pil = time.perf_counter() - t0
         ok = bool(np.allclose(np.linalg.norm(out, axis=1), 1.0, atol=1e-5))
+        index_image = index_image_leg(paths, n_images / t_all)
     finally:
         shutil.rmtree(d, ignore_errors=True)
         # the drop-in's CLIP handles go, so later legs' handles are the process's only ones (a sole
         # image handle splits a large batch into two lanes, encoder.hip)
         emb_mod._CLIP_MODEL = None
         gc.collect()
-    return {
+    return index_image, {
         "images_per_s": round(n_images / t_all, 1),
         "ms_per_256": round(t_all / n_images * 256 * 1e3, 3),
         "calls_images_per_s": [round(n_images / t, 1) for t in calls],
@@ -560,6 +561,187 @@ def ingest_leg(n_images: int = 2048):
         "workload": f"{n_images} synthetic files (3/4 JPEG q90, 1/4 PNG; 640x480 .. 1024x768; "
                     f"{nbytes / 1e6:.1f} MB on disk), embed_images_batch(paths) in batches of 256; "
                     f"images_per_s = median of three calls",
+    }
+
+
+class _BenchStore:
+    """app.ml.index_build pointed at a fresh persistent LanceDBStore in a temp directory (the drop-in
+    store: Parquet + fp32 segments on disk, rows on the GPU), restored on exit."""
+
+    def __enter__(self):
+        import tempfile
+        from pathlib import Path
+
+        from app.ml import index_build as ib
+        from app.storage.lancedb_store import LanceDBStore
+
+        self.ib, self.dir = ib, tempfile.mkdtemp(prefix="mrag_bench_index_")
+        self.saved = (ib._LANCEDB_STORE, ib._VERSION_FILE, os.environ.get("MRAG_STORE_PERSIST"))
+        os.environ["MRAG_STORE_PERSIST"] = "1"  # the retrieve leg turns persistence off for its tables
+        self.store = LanceDBStore(self.dir)
+        ib._LANCEDB_STORE, ib._VERSION_FILE = self.store, Path(self.dir) / "index_versions.json"
+        return self
+
+    def __exit__(self, *exc):
+        import shutil
+
+        ib = self.ib
+        ib._LANCEDB_STORE, ib._VERSION_FILE, persist = self.saved
+        if persist is None:
+            os.environ.pop("MRAG_STORE_PERSIST", None)
+        else:
+            os.environ["MRAG_STORE_PERSIST"] = persist
+        for t in (self.store._text_table, self.store._image_table):
+            if t.index is not None:
+                t.index.close()
+                t.index = None
+        shutil.rmtree(self.dir, ignore_errors=True)
+
+
+def _split_store(store_table, rows, modality: str):
+    """The store half of an index_*_nodes call alone, over the call's own rows: the array prepare
+    (_prepare_rows_array: the reference's _normalize bytes + json meta), the Parquet / fp32 segment
+    append, and the GPU add (each part on fresh chunk ids)."""
+    import tempfile
+
+    import numpy as np
+
+    from app.storage.corpus_files import CorpusFiles
+    from app.storage.lancedb_store import LanceDBStore
+    from app.vector_store import FlatIndex
+
+    t0 = time.perf_counter()
+    payloads, vectors = LanceDBStore._prepare_rows_array(rows)
+    t_prep = time.perf_counter() - t0
+    d = tempfile.mkdtemp(prefix="mrag_bench_seg_")
+    try:
+        cf = CorpusFiles(d)
+        t0 = time.perf_counter()
+        cf.append(vectors, payloads)
+        t_files = time.perf_counter() - t0
+    finally:
+        import shutil
+
+        shutil.rmtree(d, ignore_errors=True)
+    ix = FlatIndex(vectors.shape[1], device=store_table.device)
+    ix.add(vectors[:64], np.zeros(64, np.int32))
+    _sync()
+    t0 = time.perf_counter()
+    ix.add(vectors, np.zeros(len(vectors), np.int32))
+    _sync()
+    t_add = time.perf_counter() - t0
+    ix.close()
+    return {f"prepare_rows_array_{modality}": round(t_prep * 1e3, 3), "parquet_f32_segment_append": round(t_files * 1e3, 3),
+            "gpu_add": round(t_add * 1e3, 3)}
+
+
+def index_image_leg(paths, embed_rate: float):
+    """``index_image_nodes`` (app/ml/index_build.py -> reference app/ml/index_build.py:106-155) over
+    the ingest leg's files into a fresh persistent store: the existence checks, embed_images_batch,
+    the VectorRows, upsert_image_vectors (_normalize + json meta, the fp32 segment + Parquet
+    append, the GPU add) and the version bump. Median of three calls on fresh chunk ids, and the
+    store half's parts alone over the same rows."""
+    from app.storage.lancedb_store import VectorRow
+
+    n = len(paths)
+    with _BenchStore() as bs:
+        calls = []
+        for c in range(3):
+            nodes = [{"id": f"img{c}_{i}", "metadata": {"file_path": p, "doc_id": f"doc{i >> 4}", "source": "bench"}}
+                     for i, p in enumerate(paths)]
+            _sync()
+            t0 = time.perf_counter()
+            out = bs.ib.index_image_nodes("u0", nodes)
+            _sync()
+            calls.append(time.perf_counter() - t0)
+            assert len(out) == n
+        t_call = sorted(calls)[1]
+        import numpy as np
+
+        emb = np.random.default_rng(1).standard_normal((n, 512)).astype(np.float32)
+        rows = [VectorRow(chunk_id=f"s{i}", user_id="u0", document_id=f"doc{i >> 4}", modality="image",
+                          embedding=emb[i], meta={"file_path": p, "doc_id": f"doc{i >> 4}", "user_id": "u0",
+                                                  "modality": "image", "source": "bench"})
+                for i, p in enumerate(paths)]
+        split = _split_store(bs.store._image_table, rows, "image")
+        rows_total = len(bs.store._image_table.index)
+    store_ms = sum(split.values())
+    return {
+        "images_per_s": round(n / t_call, 1),
+        "calls_images_per_s": [round(n / t, 1) for t in calls],
+        "ratio_to_embed_images_batch": round(n / t_call / embed_rate, 3),
+        "split_ms": dict(split, embed_images_batch=round(n / embed_rate * 1e3, 3)),
+        "store_half_frac_of_call": round(store_ms / (t_call * 1e3), 3),
+        "rows_in_table": rows_total,
+        "workload": f"index_image_nodes('u0', {n} nodes) over the ingest leg's files, fresh persistent store, "
+                    "fresh chunk ids per call; median of three calls; split = each part alone",
+    }
+
+
+def _synthetic_documents(n: int, seed: int = 11):
+    import numpy as np
+
+    words = ["gpu", "vector", "search", "image", "caption", "lecture", "slide", "graph", "diagram", "model",
+             "embedding", "retrieval", "page", "figure", "table", "network", "matrix", "energy", "cell", "river",
+             "the", "of", "and", "a", "to", "in", "is", "for", "on", "with"]
+    rng = np.random.default_rng(seed)
+    docs = []
+    for i in range(n):
+        sents = []
+        for _ in range(int(rng.integers(6, 40))):
+            w = rng.choice(words, int(rng.integers(6, 18)))
+            sents.append(" ".join(w).capitalize() + ".")
+        docs.append({"id": f"doc{i}", "text": " ".join(sents), "metadata": {"source": "pdf", "page_no": int(i % 50)}})
+    return docs
+
+
+def index_text_leg(n_docs: int = 1000):
+    """``index_text_nodes`` (reference app/ml/index_build.py:46-103) over n_docs synthetic documents
+    (6-40 sentences each) into a fresh persistent store: SentenceSplitter(512/64) with the
+    metadata prefix, embed_text_batch (MiniLM-L6 on the GPU), VectorRows, upsert_text_vectors, the
+    version bump. Median of three calls on fresh document ids, and each part alone."""
+    from app.ml import index_build as ib
+    from app.ml.splitter import Document
+    from app.storage.lancedb_store import VectorRow
+
+    with _BenchStore() as bs:
+        ib.index_text_nodes("u0", _synthetic_documents(64, seed=99))  # warm: model, workspaces
+        calls, chunks = [], 0
+        for c in range(3):
+            docs = _synthetic_documents(n_docs)
+            for d in docs:
+                d["id"] = f"c{c}_{d['id']}"
+            _sync()
+            t0 = time.perf_counter()
+            out = ib.index_text_nodes("u0", docs)
+            _sync()
+            calls.append(time.perf_counter() - t0)
+            chunks = len(out)
+        t_call = sorted(calls)[1]
+        docs = _synthetic_documents(n_docs)
+        documents = [Document(text=d["text"], metadata=dict(d["metadata"]), doc_id=d["id"]) for d in docs]
+        t0 = time.perf_counter()
+        nodes = ib._SPLITTER.get_nodes_from_documents(documents)
+        texts = [nd.get_content(metadata_mode="all") for nd in nodes]
+        t_split = time.perf_counter() - t0
+        _sync()
+        t0 = time.perf_counter()
+        emb = ib.embed_text_batch(texts)
+        _sync()
+        t_embed = time.perf_counter() - t0
+        rows = [VectorRow(chunk_id=f"s{i}", user_id="u0", document_id=f"doc{i}", modality="text", embedding=emb[i],
+                          meta={"doc_id": f"doc{i}", "user_id": "u0", "modality": "text", "source": "pdf"})
+                for i in range(len(texts))]
+        split = _split_store(bs.store._text_table, rows, "text")
+    return {
+        "documents_per_s": round(n_docs / t_call, 1),
+        "chunks_per_s": round(chunks / t_call, 1),
+        "chunks_per_call": chunks,
+        "calls_documents_per_s": [round(n_docs / t, 1) for t in calls],
+        "split_ms": dict(split, sentence_splitter=round(t_split * 1e3, 3), embed_text_batch=round(t_embed * 1e3, 3)),
+        "store_half_frac_of_call": round(sum(split.values()) / (t_call * 1e3), 3),
+        "workload": f"index_text_nodes('u0', {n_docs} synthetic documents of 6-40 sentences), fresh persistent store, "
+                    "fresh document ids per call; median of three calls; split = each part alone",
     }
 
 
@@ -1016,7 +1198,9 @@ def main():
             },
         }
         if world == 1 and not args.no_ingest:
-            out["call_pattern"] = dict(call_pattern or {}, ingest_embed_images_batch=ingest_leg())
+            index_image, ingest = ingest_leg()
+            out["call_pattern"] = dict(call_pattern or {}, ingest_embed_images_batch=ingest,
+                                       index_image_nodes=index_image, index_text_nodes=index_text_leg())
             call_pattern = out["call_pattern"]
         if not args.no_clip:
             clip = clip_leg(steps=max(30, args.steps), warmup=3)  # single-GPU leg, rank 0; 30+ batches: three in flight reach steady state

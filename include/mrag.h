@@ -257,13 +257,17 @@ int mrag_png_unfilter(const uint8_t* const* raws, const int32_t* dims, int32_t n
  * embed_images_batch, app/ml/embeddings.py:82-89): mrag_files_prepare reads n files on `threads`
  * host threads of its own and classifies each — kind 1: a JPEG K13 decodes, 2: a PNG K14
  * reconstructs (inflated here), 0: anything else (decode it with Pillow), -1: unreadable (open it
- * yourself to get the error); device_decode = 0 classifies every readable file as 0.
+ * yourself to get the error); device_decode = 0 classifies every readable file as 0. A file of
+ * more than max_pixels pixels (max(1, w) * max(1, h), Pillow's decompression-bomb count) is kind 0
+ * too, so Pillow warns or raises DecompressionBombError for it as in the reference; pass Pillow's
+ * Image.MAX_IMAGE_PIXELS, or max_pixels < 0 for no limit (MAX_IMAGE_PIXELS = None).
  * mrag_files_info: kind / width / height per file (arrays of n). mrag_files_bytes: a file's bytes
  * (valid until mrag_files_free). mrag_files_decode: K13 + K14 for the kind 1 / 2 files into
  * device memory `out`, file i as H x W x 3 u8 RGB at out_offsets[i] (host array of n; entries of
  * other kinds unused); synchronous on `stream`. */
 typedef struct mrag_files mrag_files;
-int mrag_files_prepare(const char* const* paths, int32_t n, int32_t threads, int32_t device_decode, mrag_files** out);
+int mrag_files_prepare(const char* const* paths, int32_t n, int32_t threads, int32_t device_decode,
+                       int64_t max_pixels, mrag_files** out);
 int mrag_files_info(const mrag_files* files, int32_t* kind, int32_t* width, int32_t* height);
 int mrag_files_bytes(const mrag_files* files, int32_t i, const uint8_t** data, int64_t* size);
 int mrag_files_decode(const mrag_files* files, uint8_t* out, const int64_t* out_offsets, int32_t device, void* stream);

@@ -51,7 +51,7 @@ SIGNATURES = {
                                 ctypes.POINTER(_c_i64)]),
     "mrag_png_inflate": (_c_int, [ctypes.c_char_p, _c_i64, _vp, _c_i64, ctypes.POINTER(_c_int)]),
     "mrag_png_unfilter": (_c_int, [_vp, _vp, _c_int, _vp, _vp, _c_int, _vp]),
-    "mrag_files_prepare": (_c_int, [_vp, _c_int, _c_int, _c_int, ctypes.POINTER(_vp)]),
+    "mrag_files_prepare": (_c_int, [_vp, _c_int, _c_int, _c_int, _c_i64, ctypes.POINTER(_vp)]),
     "mrag_files_info": (_c_int, [_vp, _vp, _vp, _vp]),
     "mrag_files_bytes": (_c_int, [_vp, _c_int, ctypes.POINTER(_vp), ctypes.POINTER(_c_i64)]),
     "mrag_files_decode": (_c_int, [_vp, _vp, _vp, _c_int, _vp]),

@@ -157,6 +157,19 @@ def decode_batch(items: Sequence[Union[str, Path, Image.Image]]) -> List[np.ndar
 _PNG_SIG = b"\x89PNG\r\n\x1a\n"
 
 
+def max_pixels() -> int:
+    """Pillow's decompression-bomb limit as read at call time (``Image.MAX_IMAGE_PIXELS``; -1 for
+    None = no limit). A file above it is left to Pillow, which warns (or raises
+    DecompressionBombError above twice the limit) exactly as the reference's Image.open does."""
+    m = Image.MAX_IMAGE_PIXELS
+    return -1 if m is None else int(m)
+
+
+def _over_limit(w: int, h: int) -> bool:
+    m = max_pixels()
+    return m >= 0 and max(1, w) * max(1, h) > m
+
+
 def _prepare_one(x):
     """The host half for one item: a JPEG K13 decodes -> ("jpeg", file bytes, (h, w), 0), None; a
     PNG K14 reconstructs -> ("png", inflated scanlines, (h, w), bytes per pixel), None; anything
@@ -171,11 +184,13 @@ def _prepare_one(x):
 
         w, h = ctypes.c_int32(0), ctypes.c_int32(0)
         if b[:2] == b"\xff\xd8":
-            if _native.load().mrag_jpeg_probe(b, len(b), ctypes.byref(w), ctypes.byref(h)) == 1:
+            if (_native.load().mrag_jpeg_probe(b, len(b), ctypes.byref(w), ctypes.byref(h)) == 1
+                    and not _over_limit(w.value, h.value)):
                 return ("jpeg", b, (h.value, w.value), 0), None
         elif b[:8] == _PNG_SIG:
             lib, nraw = _native.load(), ctypes.c_int64(0)
-            if lib.mrag_png_probe(b, len(b), ctypes.byref(w), ctypes.byref(h), ctypes.byref(nraw)) == 1:
+            if (lib.mrag_png_probe(b, len(b), ctypes.byref(w), ctypes.byref(h), ctypes.byref(nraw)) == 1
+                    and not _over_limit(w.value, h.value)):
                 raw = np.empty(nraw.value, dtype=np.uint8)
                 bpp = ctypes.c_int32(0)
                 if lib.mrag_png_inflate(b, len(b), raw.ctypes.data, nraw.value, ctypes.byref(bpp)) == 1:
@@ -199,15 +214,16 @@ class NativePrepared:
         h = ctypes.c_void_p()
         dev = 0 if os.environ.get("MRAG_HOST_DECODE") == "1" else 1
         _native.call("mrag_files_prepare", ctypes.cast(names, ctypes.c_void_p), n, decode_workers(), dev,
-                     ctypes.byref(h))
+                     max_pixels(), ctypes.byref(h))
         self._lib, self.handle = lib, h
         kind, w, hh = (np.zeros(n, np.int32) for _ in range(3))
         _native.call("mrag_files_info", h, kind.ctypes.data, w.ctypes.data, hh.ctypes.data)
         self.kind = kind
         self.dims = np.stack([hh, w], axis=1).astype(np.int64)
         self.host: dict = {}
-        for i in np.nonzero(kind <= 0)[0]:
-            i = int(i)
+        left = [int(i) for i in np.nonzero(kind <= 0)[0]]
+
+        def host_decode(i: int) -> np.ndarray:
             if kind[i] < 0:  # the reference's error for this path (or, if it reads now, its decode)
                 with open(paths[i], "rb") as f:
                     b = f.read()
@@ -216,7 +232,13 @@ class NativePrepared:
                 _native.call("mrag_files_bytes", h, i, ctypes.byref(ptr), ctypes.byref(size))
                 b = ctypes.string_at(ptr.value, size.value) if size.value else b""
             with Image.open(io.BytesIO(b)) as im:
-                a = np.asarray(im.convert("RGB"), dtype=np.uint8)
+                return np.asarray(im.convert("RGB"), dtype=np.uint8)
+
+        # Pillow's decoders release the interpreter lock: the files the GPU decoders leave (progressive
+        # JPEGs, palette PNGs, WebP ...) decode on the process-wide pool; map keeps their order and
+        # raises the first failing file's exception, as the per-file loop would
+        decoded = list(_pool().map(host_decode, left)) if len(left) > 1 else [host_decode(i) for i in left]
+        for i, a in zip(left, decoded):
             self.host[i] = a
             self.dims[i] = a.shape[:2]
 

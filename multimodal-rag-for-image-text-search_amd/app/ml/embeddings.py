@@ -25,10 +25,9 @@ from app.settings import settings
 
 _TEXT_MODEL: Optional[Any] = None
 _DECODE_GROUP_BATCHES = 1  # encoder batches per K13 decode launch (profiles/r5s18_ingest_group_ab.jsonl)
-_PREP_PER_FILE = False  # False: one prepare_batch per group, two groups ahead — for path lists one
-# library call (preprocess.NativePrepared; profiles/r5s37_native_ab.jsonl: 16.6-18.2k img/s vs
-# 11.4-12.8k per file, three interleaved rounds). True: the host half per file on the decode pool
-# (the better of the two Python host halves: profiles/r5s35_prep_ab.jsonl, 11.2k vs 10.3k img/s)
+# The host half runs as one prepare_batch per group, two groups ahead — for path lists one library
+# call (preprocess.NativePrepared; profiles/r5s37_native_ab.jsonl: 16.6-18.2k img/s against
+# 11.4-12.8k for a per-file host half on the decode pool, three interleaved rounds)
 _CLIP_MODEL: Optional[Any] = None
 _CLIP_PROCESSOR: Optional[Any] = None
 
@@ -146,41 +145,12 @@ def embed_images_batch(paths: Sequence[Path], batch_size: int = 8) -> np.ndarray
 
                     decs[i] = dec_ex.submit(run)
 
-            files = None
-            if _PREP_PER_FILE:
-                # the host half per file on the decode pool, up to two groups ahead of the decode:
-                # no barrier at group ends (a PNG inflates ~10x longer than a JPEG is probed)
-                from app.encoders import preprocess as _pp
-
-                pool = _pp._pool()
-                files = {}
-
-                def prep(i):  # noqa: F811
-                    if i < len(starts) and i not in preps:
-                        futs = [pool.submit(_pp._prepare_one, p) for p in paths[starts[i]:starts[i] + group]]
-                        files[i] = futs
-                        preps[i] = True
-
-                def dec(i):  # noqa: F811
-                    if i < len(starts) and i not in decs:
-                        prep(i)
-                        futs = files[i]
-
-                        def run():
-                            prepared = [f.result() for f in futs]
-                            with torch.cuda.stream(dstream):
-                                return len(prepared), processor.decode_device(prepared)
-
-                        decs[i] = dec_ex.submit(run)
-
             for i in range(len(starts)):
                 dec(i)
                 dec(i + 1)
                 prep(i + 2)
                 n_i, imgs = decs.pop(i).result()
                 preps.pop(i, None)
-                if files is not None:
-                    files.pop(i, None)
                 for c0 in range(0, n_i, step):
                     inputs = processor.from_device(imgs, c0, step)
                     out.append(_to_numpy(model.get_image_features(**_kwargs(inputs))))

@@ -17,6 +17,8 @@ import threading
 from pathlib import Path
 from typing import Dict, List, Sequence
 
+import numpy as np
+
 from app.ml.embeddings import embed_images_batch, embed_query_for_images, embed_text_batch
 from app.ml.splitter import Document, SentenceSplitter
 from app.settings import settings
@@ -56,6 +58,20 @@ def get_index_version(user_id: str) -> int:
     return _load_versions().get(user_id, 0)
 
 
+def _array_rows() -> bool:
+    """True when ``_LANCEDB_STORE`` is this package's store, which takes the embeddings as numpy
+    rows and prepares them as one array (LanceDBStore._prepare_rows_array: the same vector bytes
+    as the per-row lists). Any other store (a test's stand-in) gets the reference's
+    ``embedding.tolist()`` lists (reference app/ml/index_build.py:90,151)."""
+    return isinstance(_LANCEDB_STORE, LanceDBStore)
+
+
+def _row_embedding(embedding, array_rows: bool):
+    if array_rows and isinstance(embedding, np.ndarray):
+        return embedding
+    return embedding.tolist()
+
+
 def index_text_nodes(user_id: str, nodes: Sequence[Dict[str, object]]) -> List[Dict[str, object]]:
     """Chunk and index text nodes ({id, text, metadata})."""
     documents: List[Document] = []
@@ -71,6 +87,7 @@ def index_text_nodes(user_id: str, nodes: Sequence[Dict[str, object]]) -> List[D
     if not texts:
         return []
     embeddings = embed_text_batch(texts)
+    array_rows = _array_rows()
     rows: List[VectorRow] = []
     stored: List[Dict[str, object]] = []
     for parsed, embedding in zip(parsed_nodes, embeddings):
@@ -78,7 +95,7 @@ def index_text_nodes(user_id: str, nodes: Sequence[Dict[str, object]]) -> List[D
         meta.update({"doc_id": parsed.ref_doc_id or parsed.node_id, "user_id": user_id, "modality": "text",
                      "source": meta.get("source")})
         rows.append(VectorRow(chunk_id=parsed.node_id, user_id=user_id, document_id=meta["doc_id"], modality="text",
-                              embedding=embedding.tolist(), meta=meta))
+                              embedding=_row_embedding(embedding, array_rows), meta=meta))
         stored.append({"chunk_id": parsed.node_id, "metadata": meta, "text": parsed.get_content(metadata_mode="none")})
     if rows:
         _LANCEDB_STORE.upsert_text_vectors(rows)
@@ -104,8 +121,9 @@ def index_image_nodes(user_id: str, nodes: Sequence[Dict[str, object]]) -> List[
     if not rows:
         return []
     embeddings = embed_images_batch(paths)
+    array_rows = _array_rows()
     for row, embedding in zip(rows, embeddings):
-        row.embedding = embedding.tolist()
+        row.embedding = _row_embedding(embedding, array_rows)
     _LANCEDB_STORE.upsert_image_vectors(rows)
     _bump_version(user_id)
     return [{"chunk_id": row.chunk_id, "metadata": row.meta} for row in rows]

@@ -117,11 +117,16 @@ class _Table:
 
     _load = _sync  # name used by app.retrieval
 
-    def upsert(self, payloads: List[Dict[str, Any]]) -> None:
+    def upsert(self, payloads: List[Dict[str, Any]], vectors: Optional[np.ndarray] = None) -> None:
+        """Per-row delete of the payloads' chunk ids, then one append. ``vectors`` (f32 [n, dim]):
+        the payloads' embeddings already stacked (the array path of LanceDBStore._upsert)."""
         if not payloads:
             return
         with self.lock:
-            emb = np.asarray([p["embedding"] for p in payloads], dtype=np.float32)
+            if vectors is not None:
+                emb = np.ascontiguousarray(vectors, dtype=np.float32)
+            else:
+                emb = np.asarray([p["embedding"] for p in payloads], dtype=np.float32)
             if emb.ndim != 2:
                 raise ValueError("all embeddings in one upsert must have the same length")
             with (self.files.write_lock() if self.files is not None else contextlib.nullcontext()):
@@ -207,11 +212,49 @@ class LanceDBStore:
             for row in rows
         ]
 
+    @staticmethod
+    def _normalize_rows(vectors: np.ndarray) -> np.ndarray:
+        """``_normalize`` of every row of an f32 [n, dim] array at once, bit for bit: the same
+        np.linalg.norm per row (its dot product's summation order is BLAS's, so it is not batched),
+        then one f32 division of each row by its norm; rows of norm <= 0 stay as they are."""
+        arr = np.asarray(vectors, dtype=np.float32)
+        norms = np.array([np.linalg.norm(x) for x in arr], dtype=np.float32).reshape(-1, 1)
+        out = arr / np.where(norms <= 0, np.float32(1), norms)
+        return np.where(norms <= 0, arr, out)
+
+    @staticmethod
+    def _prepare_rows_array(rows: List[VectorRow]):
+        """``_prepare_rows`` for rows whose embeddings are numpy rows (what index_text_nodes /
+        index_image_nodes hand this store): the same payload dicts and vector bytes with the
+        vectors kept as one f32 array — no per-row list round trip (tolist, then asarray)."""
+        vectors = LanceDBStore._normalize_rows(np.stack([np.asarray(r.embedding, dtype=np.float32) for r in rows]))
+        payloads = [
+            {
+                "chunk_id": row.chunk_id,
+                "user_id": row.user_id,
+                "document_id": row.document_id,
+                "modality": row.modality,
+                "embedding": vectors[i],
+                "meta": json.dumps(row.meta or {}),
+            }
+            for i, row in enumerate(rows)
+        ]
+        return payloads, vectors
+
+    def _upsert(self, table: "_Table", rows: Iterable[VectorRow]) -> None:
+        rows = list(rows)
+        if rows and all(isinstance(r.embedding, np.ndarray) and r.embedding.ndim == 1 for r in rows) \
+                and len({r.embedding.shape[0] for r in rows}) == 1:
+            payloads, vectors = self._prepare_rows_array(rows)
+            table.upsert(payloads, vectors)
+        else:
+            table.upsert(self._prepare_rows(rows))
+
     def upsert_text_vectors(self, rows: Iterable[VectorRow]) -> None:
-        self._text_table.upsert(self._prepare_rows(rows))
+        self._upsert(self._text_table, rows)
 
     def upsert_image_vectors(self, rows: Iterable[VectorRow]) -> None:
-        self._image_table.upsert(self._prepare_rows(rows))
+        self._upsert(self._image_table, rows)
 
     def search_text(self, user_id: str, query_vec: Sequence[float], top_k: int) -> List[Dict[str, Any]]:
         return self._format_results(self._text_table.search(user_id, self._normalize(query_vec), max(top_k, 1)))

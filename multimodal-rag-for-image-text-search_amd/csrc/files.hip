@@ -113,7 +113,13 @@ bool read_file(const char* path, std::vector<uint8_t>& out) {
 }
 
 // read, then parse what K13 / K14 may take (kind 2 is provisional until the inflate succeeds)
-void classify(mrag_files& F, int i, const char* path, bool device_decode) {
+// Pillow's decompression-bomb count (Image._decompression_bomb_check): above max_pixels it warns,
+// above twice that it raises; either way the file is Pillow's (kind 0), as in the reference
+bool over_limit(int64_t w, int64_t h, int64_t max_pixels) {
+  return max_pixels >= 0 && std::max<int64_t>(1, w) * std::max<int64_t>(1, h) > max_pixels;
+}
+
+void classify(mrag_files& F, int i, const char* path, bool device_decode, int64_t max_pixels) {
   std::vector<uint8_t>& d = F.data[i];
   if (!read_file(path, d)) {
     F.kind[i] = -1;
@@ -123,14 +129,15 @@ void classify(mrag_files& F, int i, const char* path, bool device_decode) {
   if (!device_decode) return;
   const int64_t n = (int64_t)d.size();
   if (n >= 2 && d[0] == 0xFF && d[1] == 0xD8) {
-    if (mrag_jpeg::parse(d.data(), n, F.jp[i])) {
+    if (mrag_jpeg::parse(d.data(), n, F.jp[i]) &&
+        !over_limit(F.jp[i].img.width, F.jp[i].img.height, max_pixels)) {
       F.kind[i] = 1;
       F.w[i] = F.jp[i].img.width;
       F.h[i] = F.jp[i].img.height;
     }
     return;
   }
-  if (mrag_png::png_parse(d.data(), n, F.pp[i], true)) {
+  if (mrag_png::png_parse(d.data(), n, F.pp[i], true) && !over_limit(F.pp[i].width, F.pp[i].height, max_pixels)) {
     F.kind[i] = 2;
     F.w[i] = F.pp[i].width;
     F.h[i] = F.pp[i].height;
@@ -180,7 +187,8 @@ bool on_threads(int n, int threads, Fn fn) {
   return !thrown;
 }
 
-int prepare_impl(const char* const* paths, int32_t n, int32_t threads, int32_t device_decode, mrag_files** out) {
+int prepare_impl(const char* const* paths, int32_t n, int32_t threads, int32_t device_decode, int64_t max_pixels,
+                 mrag_files** out) {
   if (!out || n < 0 || (n > 0 && !paths)) return mrag::fail(MRAG_ERR_ARG, "NULL argument");
   *out = nullptr;
   auto* F = new mrag_files();
@@ -198,7 +206,7 @@ int prepare_impl(const char* const* paths, int32_t n, int32_t threads, int32_t d
   F->pp.resize((size_t)n);
   F->off.assign((size_t)n, 0);
   F->seg0.assign((size_t)n, 0);
-  if (!on_threads(n, threads, [&](int i) { classify(*F, i, paths[i], device_decode != 0); })) return fail_oom();
+  if (!on_threads(n, threads, [&](int i) { classify(*F, i, paths[i], device_decode != 0, max_pixels); })) return fail_oom();
   // the arena: every JPEG's segments (K13's stage layout, file order), then every PNG's scanlines
   int64_t pos = 0;
   int32_t nseg = 0;
@@ -265,9 +273,10 @@ int decode_impl(const mrag_files* F, uint8_t* out, const int64_t* out_offsets, i
 extern "C" {
 
 // the C ABI: no C++ exception crosses it (a failed host allocation is MRAG_ERR_OOM)
-int mrag_files_prepare(const char* const* paths, int32_t n, int32_t threads, int32_t device_decode, mrag_files** out) {
+int mrag_files_prepare(const char* const* paths, int32_t n, int32_t threads, int32_t device_decode,
+                       int64_t max_pixels, mrag_files** out) {
   try {
-    return prepare_impl(paths, n, threads, device_decode, out);
+    return prepare_impl(paths, n, threads, device_decode, max_pixels, out);
   } catch (...) {
     return mrag::fail(MRAG_ERR_OOM, "files: host allocation failed");
   }

@@ -307,6 +307,9 @@ static int jpeg_decode_impl(const uint8_t* const* files, const int64_t* sizes, i
   if (int rc = ensure(C.segs, sizeof(ParSeg) * segs.size())) return rc;
   if (int rc = ensure(C.coef, (size_t)blocks * 128)) return rc;
   if (int rc = ensure(C.planes, (size_t)planes)) return rc;
+  // an error return from here on first drains s: the copies read imgs / segs on this stack frame
+  // and the staging arena, which the caller may hand back to its pool
+  mrag::StreamDrain drain(s);
   MRAG_HIP(hipMemcpyAsync(C.ecs.p, src, (size_t)stage_bytes, hipMemcpyHostToDevice, s));
   MRAG_HIP(hipMemcpyAsync(C.imgs.p, imgs.data(), sizeof(Image) * (size_t)n, hipMemcpyHostToDevice, s));
   MRAG_HIP(hipMemcpyAsync(C.segs.p, segs.data(), sizeof(ParSeg) * segs.size(), hipMemcpyHostToDevice, s));
@@ -322,6 +325,7 @@ static int jpeg_decode_impl(const uint8_t* const* files, const int64_t* sizes, i
   MRAG_CHECK_LAUNCH();
   // the descriptors above live on this host stack frame: the copies must finish before return
   if (int rc = mrag::blocking_wait(s)) return rc;
+  drain.armed = false;
   return MRAG_OK;
 }
 

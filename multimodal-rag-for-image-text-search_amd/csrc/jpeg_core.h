@@ -189,7 +189,8 @@ struct Bits {
 __host__ __device__ inline int extend(int x, int s) { return s == 0 ? 0 : (x < (1 << (s - 1)) ? x - (1 << s) + 1 : x); }
 
 // Decode one 8x8 block: DC predictor in/out, coefficients (natural order, not dequantized) out.
-// An AC run past index 63 (corrupt data) is dropped, as libjpeg drops it.
+// An AC run past index 63 (corrupt data: k up to 63 + 15) lands on natural index 63, as in libjpeg,
+// whose jpeg_natural_order[] carries 16 extra entries of 63 for exactly this (jdhuff.c).
 __host__ __device__ inline void decode_block(Bits& br, const Huff& dc, const Huff& ac, int& pred, int16_t* coef) {
   const int s = br.decode(dc);
   if (br.cnt < 16) br.fill();
@@ -203,7 +204,7 @@ __host__ __device__ inline void decode_block(Bits& br, const Huff& dc, const Huf
       k += r;
       if (br.cnt < 16) br.fill();
       const int v = extend((int)br.get(sz), sz);
-      if (k < 64) coef[zigzag(k)] = (int16_t)v;
+      coef[k < 64 ? zigzag(k) : 63] = (int16_t)v;
       ++k;
     } else {
       if (r != 15) break;  // EOB
@@ -442,7 +443,7 @@ __host__ __device__ inline bool par_run(const TAB& T, PBits& br, PState& st, uin
       const int r = sym >> 4;
       if (s) {
         k += r;
-        if (MODE == PAR_WRITE && k < 64) coef[blk * 64 + zigzag(k)] = (int16_t)extend((int)v, s);
+        if (MODE == PAR_WRITE) coef[blk * 64 + (k < 64 ? zigzag(k) : 63)] = (int16_t)extend((int)v, s);
         ++k;
       } else if (r == 15) {
         k += 16;

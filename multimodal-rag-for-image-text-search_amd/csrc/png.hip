@@ -256,6 +256,9 @@ static int png_unfilter_impl(const uint8_t* const* raws, const int32_t* dims, in
   }
   if (int rc = ensure(C.raw, (size_t)total)) return rc;
   if (int rc = ensure(C.imgs, sizeof(PngImg) * (size_t)n)) return rc;
+  // an error return from here on first drains s: the copies read imgs on this stack frame and the
+  // staging buffer, which the caller may hand back to its pool
+  mrag::StreamDrain drain(s);
   MRAG_HIP(hipMemcpyAsync(C.raw.p, staged ? staged : C.stage, (size_t)total, hipMemcpyHostToDevice, s));
   MRAG_HIP(hipMemcpyAsync(C.imgs.p, imgs.data(), sizeof(PngImg) * (size_t)n, hipMemcpyHostToDevice, s));
   // one launch per pixel size present (a workgroup of another size returns at once)
@@ -271,6 +274,7 @@ static int png_unfilter_impl(const uint8_t* const* raws, const int32_t* dims, in
   if (has[4]) launch(png_unfilter_kernel<4>);
   MRAG_CHECK_LAUNCH();
   if (int rc = mrag::blocking_wait(s)) return rc;  // the descriptors live on this stack frame
+  drain.armed = false;
   return MRAG_OK;
 }
 

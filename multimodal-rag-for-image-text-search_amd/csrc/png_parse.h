@@ -37,7 +37,7 @@ inline bool png_parse(const uint8_t* d, int64_t n, PngParsed& P, bool check_crc)
   static const uint8_t sig[8] = {0x89, 'P', 'N', 'G', 0x0D, 0x0A, 0x1A, 0x0A};
   if (n < 8 || std::memcmp(d, sig, 8) != 0) return png_fail(P, "not a PNG");
   int64_t pos = 8;
-  bool ihdr = false, iend = false;
+  bool ihdr = false, iend = false, idat_gap = false;
   while (pos + 12 <= n) {
     const int64_t len = be32(d + pos);
     const uint8_t* type = d + pos + 4;
@@ -66,10 +66,16 @@ inline bool png_parse(const uint8_t* d, int64_t n, PngParsed& P, bool check_crc)
     } else if (!ihdr) {
       return png_fail(P, "IHDR not first");
     } else if (std::memcmp(type, "IDAT", 4) == 0) {
+      // Pillow reads only the first run of consecutive IDAT chunks (PngImageFile.load_read stops
+      // at the next other chunk: "image file is truncated" if scanlines are still missing), so a
+      // file with a second run goes to Pillow, which decides what it is
+      if (idat_gap) return png_fail(P, "IDAT chunks not consecutive");
       P.idat.emplace_back(pos + 8, len);
     } else if (std::memcmp(type, "IEND", 4) == 0) {
       iend = true;
       break;
+    } else if (!P.idat.empty()) {
+      idat_gap = true;
     }
     pos += 12 + len;
   }

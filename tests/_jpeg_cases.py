@@ -74,6 +74,94 @@ def damaged_cases():
     return out
 
 
+def _segments(b: bytes):
+    """(marker, payload start, payload end) of every marker segment before the scan data."""
+    i = 2
+    while i + 4 <= len(b):
+        marker, seglen = b[i + 1], int.from_bytes(b[i + 2:i + 4], "big")
+        yield marker, i + 4, i + 2 + seglen
+        if marker == 0xDA:
+            return
+        i += 2 + seglen
+
+
+def _huffman_codes(b: bytes):
+    """{(table class, id): {symbol: (code, length)}} from the file's DHT segments (canonical codes,
+    JPEG Annex C)."""
+    tables = {}
+    for marker, lo, hi in _segments(b):
+        if marker != 0xC4:
+            continue
+        p = lo
+        while p < hi:
+            tc, th = b[p] >> 4, b[p] & 15
+            counts = b[p + 1:p + 17]
+            syms = b[p + 17:p + 17 + sum(counts)]
+            code, k, codes = 0, 0, {}
+            for length in range(1, 17):
+                for _ in range(counts[length - 1]):
+                    codes[syms[k]] = (code, length)
+                    code, k = code + 1, k + 1
+                code <<= 1
+            tables[(tc, th)] = codes
+            p += 17 + sum(counts)
+    return tables
+
+
+def overlong_run_cases():
+    """Grayscale files whose entropy-coded data holds AC runs past coefficient 63 (corrupt data:
+    after a ZRL chain a run/size token lands on k = 64..78). libjpeg-turbo writes such a value to
+    natural index 63 (jpeg_natural_order[] carries 16 extra 63 entries, jdhuff.c); every other
+    block decodes normally. The scan is re-encoded with the file's own (standard) Huffman tables."""
+    base = jpeg_bytes(photo(16, 24, 7)[..., 0], quality=90)
+    codes = _huffman_codes(base)
+    dc, ac = codes[(0, 0)], codes[(1, 0)]
+    sos_end = max(hi for m, lo, hi in _segments(base) if m == 0xDA)
+
+    def amp(v):  # (size category, extra bits) of a coefficient value (F.1.2.1)
+        n = abs(v).bit_length()
+        return n, (v if v > 0 else v + (1 << n) - 1)
+
+    out = []
+    # one token list per block of the 3 x 2 blocks: (table, symbol, value or None)
+    plans = {
+        "overlong_r15_s2": [[("dc", 5), ("ac", 0xF0), ("ac", 0xF0), ("ac", 0xF0), ("acv", 15, 3)],
+                            [("dc", 0), ("acv", 0, 1), ("ac", 0x00)]],
+        "overlong_k60_then_76": [[("dc", -3), ("ac", 0xF0), ("ac", 0xF0), ("ac", 0xF0), ("acv", 10, -2),
+                                  ("acv", 15, 7)], [("dc", 2), ("acv", 2, -1), ("ac", 0x00)]],
+        "overlong_exact_63": [[("dc", 1), ("ac", 0xF0), ("ac", 0xF0), ("ac", 0xF0), ("acv", 14, 9)],
+                              [("dc", 0), ("ac", 0x00)]],
+    }
+    for name, plan in plans.items():
+        bits = []
+
+        def put(code, length):
+            bits.extend((code >> (length - 1 - j)) & 1 for j in range(length))
+
+        for blk in range(6):
+            for tok in plan[blk % len(plan)]:
+                if tok[0] == "dc":
+                    cat, extra = amp(tok[1]) if tok[1] else (0, 0)
+                    put(*dc[cat])
+                    if cat:
+                        put(extra, cat)
+                elif tok[0] == "ac":
+                    put(*ac[tok[1]])
+                else:
+                    cat, extra = amp(tok[2])
+                    put(*ac[(tok[1] << 4) | cat])
+                    put(extra, cat)
+        bits.extend([1] * (-len(bits) % 8))
+        data = bytearray()
+        for i in range(0, len(bits), 8):
+            v = int("".join(map(str, bits[i:i + 8])), 2)
+            data.append(v)
+            if v == 0xFF:
+                data.append(0)
+        out.append((name, base[:sos_end] + bytes(data) + b"\xff\xd9"))
+    return out
+
+
 def pillow_rgb(b: bytes) -> np.ndarray:
     with Image.open(io.BytesIO(b)) as im:
         return np.asarray(im.convert("RGB"), dtype=np.uint8)

@@ -123,6 +123,30 @@ def truncated_stream_case():
     return b"\x89PNG\r\n\x1a\n" + _chunk(b"IHDR", ihdr) + _chunk(b"IDAT", data) + _chunk(b"IEND", b"")
 
 
+def split_idat_case(tail_complete: bool = False) -> bytes:
+    """A PNG whose IDAT chunks are not consecutive (a tEXt chunk between two runs). Pillow reads
+    only the first run (PngImageFile.load_read stops at the other chunk) and raises "image file is
+    truncated" when scanlines are still missing, so K14 must leave such a file to Pillow.
+    tail_complete: the first run already holds the whole stream (the second IDAT is empty), which
+    Pillow decodes — K14 refuses it as well and Pillow decides."""
+    pix = _content(40, 30, 3, False)
+    b = filtered_png(pix, 2, idat_size=1 << 20 if tail_complete else 300)
+    sig, rest = b[:8], b[8:]
+    chunks, p = [], 0
+    while p < len(rest):
+        n = int.from_bytes(rest[p:p + 4], "big")
+        chunks.append(rest[p:p + 12 + n])
+        p += 12 + n
+    idat = [i for i, c in enumerate(chunks) if c[4:8] == b"IDAT"]
+    text = _chunk(b"tEXt", b"k\0v")
+    if tail_complete:
+        chunks.insert(idat[-1] + 1, text + _chunk(b"IDAT", b""))
+    else:
+        assert len(idat) >= 2
+        chunks.insert(idat[0] + 1, text)
+    return sig + b"".join(chunks)
+
+
 def pillow_rgb(b: bytes) -> np.ndarray:
     with Image.open(io.BytesIO(b)) as im:
         return np.asarray(im.convert("RGB"), dtype=np.uint8)

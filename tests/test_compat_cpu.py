@@ -217,6 +217,54 @@ def test_index_image_nodes(monkeypatch, tmp_path):
              {"id": "img-2", "metadata": {"file_path": str(tmp_path / "missing.png")}}]
     indexed = index_build.index_image_nodes("user-1", nodes)
     assert [i["chunk_id"] for i in indexed] == ["img-1"] and len(store.image_rows) == 1
+    assert isinstance(store.image_rows[0].embedding, list)  # a foreign store gets the reference's lists
+
+
+def test_normalize_rows_bit_identical_to_normalize():
+    """LanceDBStore._normalize_rows (the array path index_*_nodes take into this store) gives the
+    bytes of the reference's per-vector _normalize (app/storage/lancedb_store.py:63-69) on every
+    row: un-normalised, tiny, huge, zero and NaN rows."""
+    from app.storage.lancedb_store import LanceDBStore
+
+    rng = np.random.default_rng(3)
+    e = rng.standard_normal((300, 512)).astype(np.float32) * rng.uniform(1e-3, 1e3, (300, 1)).astype(np.float32)
+    e[5] = 0
+    e[6, 3] = np.nan
+    e[7] *= np.float32(1e-20)
+    e[8] *= np.float32(1e18)
+    got = LanceDBStore._normalize_rows(e)
+    assert got.dtype == np.float32
+    for i in range(len(e)):
+        want = np.asarray(LanceDBStore._normalize(e[i].tolist()), dtype=np.float32)
+        assert want.tobytes() == got[i].tobytes(), i
+
+
+def test_prepare_rows_array_equals_list_path():
+    """The array path's payloads equal _prepare_rows' (the reference's helper) field for field, the
+    vectors byte for byte; the store dispatches numpy-row embeddings to it and lists to the
+    reference's helper."""
+    from app.storage.lancedb_store import LanceDBStore, VectorRow
+
+    rng = np.random.default_rng(4)
+    e = rng.standard_normal((64, 384)).astype(np.float32)
+    rows = [VectorRow(chunk_id=f"c{i}", user_id="u", document_id=f"d{i}", modality="text", embedding=e[i],
+                      meta={"i": i, "s": "x"}) for i in range(64)]
+    payloads, vectors = LanceDBStore._prepare_rows_array(rows)
+    ref = LanceDBStore._prepare_rows([VectorRow(**{**r.__dict__, "embedding": r.embedding.tolist()}) for r in rows])
+    for p, q, v in zip(payloads, ref, vectors):
+        assert {k: p[k] for k in p if k != "embedding"} == {k: q[k] for k in q if k != "embedding"}
+        assert np.asarray(q["embedding"], np.float32).tobytes() == v.tobytes() == p["embedding"].tobytes()
+
+    class _T:
+        def upsert(self, payloads, vectors=None):
+            self.got = (payloads, vectors)
+
+    store = LanceDBStore.__new__(LanceDBStore)
+    t = _T()
+    store._upsert(t, rows)
+    assert t.got[1] is not None and t.got[1].tobytes() == vectors.tobytes()
+    store._upsert(t, [VectorRow(**{**r.__dict__, "embedding": r.embedding.tolist()}) for r in rows])
+    assert t.got[1] is None and t.got[0] == ref
 
 
 # ---------------------------------------------------------------- cache

@@ -300,7 +300,10 @@ def test_gelu_erf_epilogue_sweep(cuda):
     bound = ref.abs() * 2.0 ** -11 + 2e-6
     assert bool((err <= bound).all()), float((err - bound).max())
     neg = x < -3.5
-    record_numerics("gelu_erf_epilogue_sweep", out.float().cpu().numpy()[:1], ref.float().cpu().numpy()[:1],
+    # the recorded rows: x in [-3.5, 8), where the output is not ~0, so the cosine and the relative
+    # L2 of each 4096-wide row mean something (the rows below -3.5 are covered by the absolute bound)
+    keep = slice(36, M)  # r / 8 - 8 >= -3.5
+    record_numerics("gelu_erf_epilogue_sweep", out.float().cpu().numpy()[keep], ref.float().cpu().numpy()[keep],
                     unit=False, max_abs_err=float(err.max()), max_abs_err_x_below_m3p5=float(err[neg].max()))
 
 

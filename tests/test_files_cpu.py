@@ -6,6 +6,7 @@ the device half, is covered by the -m gpu tests)."""
 from __future__ import annotations
 
 import ctypes
+import io
 import os
 
 import numpy as np
@@ -52,7 +53,7 @@ def test_prepare_matches_per_file_probes(tmp_path, device_decode):
     n = len(paths)
     names = (ctypes.c_char_p * n)(*[os.fsencode(p) for p in paths])
     h = ctypes.c_void_p()
-    _native.call("mrag_files_prepare", ctypes.cast(names, ctypes.c_void_p), n, 4, device_decode, ctypes.byref(h))
+    _native.call("mrag_files_prepare", ctypes.cast(names, ctypes.c_void_p), n, 4, device_decode, -1, ctypes.byref(h))
     try:
         kind, w, hh = (np.zeros(n, np.int32) for _ in range(3))
         _native.call("mrag_files_info", h, kind.ctypes.data, w.ctypes.data, hh.ctypes.data)
@@ -74,9 +75,9 @@ def test_prepare_bad_arguments():
 
     lib = _native.load()
     h = ctypes.c_void_p()
-    assert lib.mrag_files_prepare(None, 3, 1, 1, ctypes.byref(h)) != 0
-    assert lib.mrag_files_prepare(None, 0, 1, 1, None) != 0
-    assert lib.mrag_files_prepare(None, 0, 1, 1, ctypes.byref(h)) == 0  # an empty group
+    assert lib.mrag_files_prepare(None, 3, 1, 1, -1, ctypes.byref(h)) != 0
+    assert lib.mrag_files_prepare(None, 0, 1, 1, -1, None) != 0
+    assert lib.mrag_files_prepare(None, 0, 1, 1, -1, ctypes.byref(h)) == 0  # an empty group
     ptr, size = ctypes.c_void_p(), ctypes.c_int64()
     assert lib.mrag_files_bytes(h, 0, ctypes.byref(ptr), ctypes.byref(size)) != 0  # index out of range
     lib.mrag_files_free(h)
@@ -103,3 +104,82 @@ def test_native_prepared_host_files(tmp_path):
     del prep
     with pytest.raises(FileNotFoundError):
         NativePrepared([items[0][0], str(tmp_path / "missing.jpg")])
+
+
+def _kinds(tmp_path, blobs, max_pixels):
+    from app import _native
+
+    lib = _native.load()
+    paths = []
+    for i, b in enumerate(blobs):
+        ext = "jpg" if b[:2] == b"\xff\xd8" else "png"
+        p = tmp_path / f"lim{i}.{ext}"
+        p.write_bytes(b)
+        paths.append(os.fsencode(str(p)))
+    names = (ctypes.c_char_p * len(paths))(*paths)
+    h = ctypes.c_void_p()
+    _native.call("mrag_files_prepare", ctypes.cast(names, ctypes.c_void_p), len(paths), 2, 1, max_pixels,
+                 ctypes.byref(h))
+    try:
+        kind, w, hh = (np.zeros(len(paths), np.int32) for _ in range(3))
+        _native.call("mrag_files_info", h, kind.ctypes.data, w.ctypes.data, hh.ctypes.data)
+        return kind.tolist()
+    finally:
+        lib.mrag_files_free(h)
+
+
+def _sof_resized(b: bytes, h: int, w: int) -> bytes:
+    """A JPEG whose frame header claims h x w (the entropy-coded data unchanged): the header a
+    decompression bomb carries."""
+    i = 2
+    while i + 4 <= len(b):
+        marker, seglen = b[i + 1], int.from_bytes(b[i + 2:i + 4], "big")
+        if marker == 0xC0:
+            return b[:i + 5] + h.to_bytes(2, "big") + w.to_bytes(2, "big") + b[i + 9:]
+        i += 2 + seglen
+    raise AssertionError("no SOF0")
+
+
+def test_prepare_pixel_limit(tmp_path):
+    """files above Pillow's decompression-bomb limit (max(1,w)*max(1,h) > MAX_IMAGE_PIXELS)
+    are kind 0, so Pillow warns / raises DecompressionBombError for them as in the reference; at or
+    below the limit, and with no limit (-1), the GPU decoders take them."""
+    from PIL import Image
+
+    jpg = J.jpeg_bytes(J.photo(48, 64, 1), quality=90)
+    png = P.supported_cases()[0][1]
+    with Image.open(io.BytesIO(png)) as im:
+        pw, ph = im.size
+    assert _kinds(tmp_path, [jpg, png], -1) == [1, 2]
+    assert _kinds(tmp_path, [jpg, png], max(48 * 64, pw * ph)) == [1, 2]
+    assert _kinds(tmp_path, [jpg, png], min(48 * 64, pw * ph) - 1) == [0, 0]
+    assert _kinds(tmp_path, [jpg, png], 0) == [0, 0]
+    bomb = _sof_resized(jpg, 20000, 20000)  # 4e8 px > 2 x Pillow's default limit
+    assert _kinds(tmp_path, [bomb], -1) == [1]
+    assert _kinds(tmp_path, [bomb], Image.MAX_IMAGE_PIXELS) == [0]
+
+
+def test_native_prepared_raises_pillows_bomb_error(tmp_path, monkeypatch):
+    """The drop-in passes Image.MAX_IMAGE_PIXELS at call time: a file above twice the limit raises
+    Pillow's DecompressionBombError (reference: Image.open(path) in embed_images_batch), one above
+    the limit decodes with Pillow's DecompressionBombWarning."""
+    import warnings
+
+    from PIL import Image
+
+    from app.encoders.preprocess import NativePrepared
+
+    p = tmp_path / "a.jpg"
+    b = J.jpeg_bytes(J.photo(48, 64, 2), quality=90)
+    p.write_bytes(b)
+    monkeypatch.setattr(Image, "MAX_IMAGE_PIXELS", 48 * 64 // 3)
+    with pytest.raises(Image.DecompressionBombError):
+        NativePrepared([str(p)])
+    monkeypatch.setattr(Image, "MAX_IMAGE_PIXELS", 48 * 64 - 1)
+    with warnings.catch_warnings(record=True) as caught:
+        warnings.simplefilter("always")
+        prep = NativePrepared([str(p)])
+    assert prep.kind[0] == 0 and any(issubclass(c.category, Image.DecompressionBombWarning) for c in caught)
+    np.testing.assert_array_equal(prep.host[0], J.pillow_rgb(b))
+    monkeypatch.setattr(Image, "MAX_IMAGE_PIXELS", None)
+    assert NativePrepared([str(p)]).kind[0] == 1

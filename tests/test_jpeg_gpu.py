@@ -10,7 +10,7 @@ import os
 import numpy as np
 import pytest
 
-from _jpeg_cases import damaged_cases, photo, pillow_rgb, supported_cases, unsupported_cases
+from _jpeg_cases import damaged_cases, overlong_run_cases, photo, pillow_rgb, supported_cases, unsupported_cases
 
 pytestmark = pytest.mark.gpu
 
@@ -34,7 +34,7 @@ def _decode_batch(cases, cuda):
 
 
 def test_decode_matches_pillow(cuda):
-    cases = supported_cases()
+    cases = supported_cases() + overlong_run_cases()  # + AC runs past 63
     got = _decode_batch(cases, cuda)  # one batch: every segment of every file in one launch
     for (name, b), g in zip(cases, got):
         np.testing.assert_array_equal(g, pillow_rgb(b), err_msg=name)
@@ -124,10 +124,12 @@ def test_damaged_files_as_pillow(cuda, tmp_path):
 
 
 def test_embed_images_batch_group_host_half_equals_per_file(cuda, tmp_path):
-    """embed_images_batch with the host half as one library call per group (_PREP_PER_FILE False:
-    processor.decode -> NativePrepared) equals the per-file submission bit for bit."""
+    """embed_images_batch with the host half as one library call per group (preprocess._NATIVE_FILES
+    True: processor.decode -> NativePrepared) equals the per-file host half (_prepare_one on the
+    decode pool) bit for bit."""
     from PIL import Image
 
+    from app.encoders import preprocess as pp
     from app.ml import embeddings as emb
 
     paths = []
@@ -136,12 +138,12 @@ def test_embed_images_batch_group_host_half_equals_per_file(cuda, tmp_path):
         p = tmp_path / (f"g{i}.png" if i % 4 == 3 else f"g{i}.jpg")
         Image.fromarray(a).save(p, **({} if i % 4 == 3 else {"quality": 85}))
         paths.append(str(p))
-    keep = emb._PREP_PER_FILE
+    keep = pp._NATIVE_FILES
     try:
-        emb._PREP_PER_FILE = True
+        pp._NATIVE_FILES = False
         per_file = emb.embed_images_batch(paths)
-        emb._PREP_PER_FILE = False
+        pp._NATIVE_FILES = True
         group = emb.embed_images_batch(paths)
     finally:
-        emb._PREP_PER_FILE = keep
+        pp._NATIVE_FILES = keep
     np.testing.assert_array_equal(group, per_file)
