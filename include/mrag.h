@@ -272,6 +272,11 @@ int mrag_files_info(const mrag_files* files, int32_t* kind, int32_t* width, int3
 int mrag_files_bytes(const mrag_files* files, int32_t i, const uint8_t** data, int64_t* size);
 int mrag_files_decode(const mrag_files* files, uint8_t* out, const int64_t* out_offsets, int32_t device, void* stream);
 int mrag_files_free(mrag_files* files);
+/* mrag_paths_exist: pathlib.Path(p).exists() for n paths at once (index_image_nodes' filter of
+ * missing files, reference app/ml/index_build.py:114-118) on `threads` host threads: out[i] = 1
+ * (stat succeeds; "" is Path("") = "."), 0 (missing: ENOENT / ENOTDIR / EBADF / ELOOP, the errors
+ * Path.exists ignores), -1 (any other error: the caller asks Path.exists, which raises it). */
+int mrag_paths_exist(const char* const* paths, int32_t n, int32_t threads, int32_t* out);
 
 /* K3 building block: C[M][N] (op)= A[M][K] . W[N][K]^T + bias (device pointers;
  * A, W fp16 row-major; epilogue 0 f16 out, 1 f16 quick_gelu, 2 f16 gelu_erf,

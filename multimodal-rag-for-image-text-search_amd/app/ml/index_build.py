@@ -28,6 +28,7 @@ _SPLITTER = SentenceSplitter(chunk_size=512, chunk_overlap=64)
 _LANCEDB_STORE = LanceDBStore(settings.paths.lancedb_dir)
 _VERSION_FILE = Path(settings.paths.lancedb_dir) / "index_versions.json"
 _VERSION_LOCK = threading.Lock()
+_EMBED_IMAGES_NATIVE = embed_images_batch  # this package's (takes str paths); tests may rebind the global
 
 
 def _load_versions() -> Dict[str, int]:
@@ -103,24 +104,79 @@ def index_text_nodes(user_id: str, nodes: Sequence[Dict[str, object]]) -> List[D
     return stored
 
 
+def _paths_exist(strs: List[str]) -> List[bool]:
+    """``Path(s).exists()`` for every s (reference app/ml/index_build.py:114-118), the stats in one
+    library call on host threads (``mrag_paths_exist``): missing -> False, an error Path.exists does
+    not ignore -> Path.exists itself raises it; a path Path cannot encode (a NUL byte) -> False."""
+    import ctypes
+
+    from app import _native
+    from app.encoders.preprocess import decode_workers
+
+    n = len(strs)
+    enc, ok = [], [True] * n
+    for i, s in enumerate(strs):
+        try:
+            b = os.fsencode(s)
+        except UnicodeError:
+            b = None
+        if b is None or b"\0" in b:  # Path.exists: ValueError -> False
+            ok[i] = False
+            b = b""
+        enc.append(b)
+    out = np.zeros(n, np.int32)
+    if n:
+        names = (ctypes.c_char_p * n)(*enc)
+        _native.call("mrag_paths_exist", ctypes.cast(names, ctypes.c_void_p), n, min(8, decode_workers()),
+                     out.ctypes.data)
+    res = []
+    for i in range(n):
+        if not ok[i]:
+            res.append(False)
+        elif out[i] < 0:
+            res.append(Path(strs[i]).exists())  # raises what the reference's check raises
+        else:
+            res.append(bool(out[i]))
+    return res
+
+
 def index_image_nodes(user_id: str, nodes: Sequence[Dict[str, object]]) -> List[Dict[str, object]]:
-    """Index image nodes ({id, metadata{file_path, ...}}) with CLIP embeddings."""
-    paths: List[Path] = []
-    rows: List[VectorRow] = []
-    for node in nodes:
-        metadata = dict(node.get("metadata", {}))
-        file_path = Path(str(metadata.get("file_path", "")))
-        if not file_path.exists():
-            continue
-        chunk_id = str(node.get("id"))
-        metadata.update({"doc_id": metadata.get("doc_id", chunk_id), "user_id": user_id, "modality": "image",
-                         "source": metadata.get("source")})
-        paths.append(file_path)
-        rows.append(VectorRow(chunk_id=chunk_id, user_id=user_id, document_id=metadata["doc_id"], modality="image",
-                              embedding=[], meta=metadata))
-    if not rows:
+    """Index image nodes ({id, metadata{file_path, ...}}) with CLIP embeddings.
+
+    The reference's per-node loop (:110-126) as three steps with the same result: the metadata
+    copies and file paths, the existence filter as one library call (_paths_exist), then the
+    VectorRows built on a helper thread while this one embeds the files (this package's
+    embed_images_batch takes the paths as strings; a substituted one gets Path objects)."""
+    metas = [dict(node.get("metadata", {})) for node in nodes]
+    strs = [str(m.get("file_path", "")) for m in metas]
+    sel = [i for i, e in enumerate(_paths_exist(strs)) if e]
+    if not sel:
         return []
-    embeddings = embed_images_batch(paths)
+    embed = embed_images_batch
+    native = embed is _EMBED_IMAGES_NATIVE
+    paths = [strs[i] for i in sel] if native else [Path(strs[i]) for i in sel]
+
+    def build_rows() -> List[VectorRow]:
+        out = []
+        for i in sel:
+            metadata = metas[i]
+            chunk_id = str(nodes[i].get("id"))
+            metadata.update({"doc_id": metadata.get("doc_id", chunk_id), "user_id": user_id, "modality": "image",
+                             "source": metadata.get("source")})
+            out.append(VectorRow(chunk_id=chunk_id, user_id=user_id, document_id=metadata["doc_id"], modality="image",
+                                 embedding=[], meta=metadata))
+        return out
+
+    if native and len(sel) >= 256:
+        from concurrent.futures import ThreadPoolExecutor
+
+        with ThreadPoolExecutor(max_workers=1) as ex:
+            fut = ex.submit(build_rows)
+            embeddings = embed(paths)
+            rows = fut.result()
+    else:
+        rows = build_rows()
+        embeddings = embed(paths)
     array_rows = _array_rows()
     for row, embedding in zip(rows, embeddings):
         row.embedding = _row_embedding(embedding, array_rows)

@@ -11,11 +11,14 @@
 #include <atomic>
 #include <cstdio>
 #include <cstdlib>
+#include <cerrno>
 #include <cstring>
 #include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
+
+#include <sys/stat.h>
 
 #include "common.h"
 #include "jpeg_parse.h"
@@ -309,6 +312,25 @@ int mrag_files_decode(const mrag_files* F, uint8_t* out, const int64_t* out_offs
 
 int mrag_files_free(mrag_files* F) {
   delete F;
+  return MRAG_OK;
+}
+
+int mrag_paths_exist(const char* const* paths, int32_t n, int32_t threads, int32_t* out) {
+  MRAG_REQUIRE(n >= 0 && (n == 0 || (paths && out)), "NULL argument");
+  try {
+    on_threads(n, threads, [&](int i) {
+      const char* p = paths[i] && paths[i][0] ? paths[i] : ".";
+      struct stat st;
+      if (stat(p, &st) == 0) {
+        out[i] = 1;
+      } else {
+        const int e = errno;
+        out[i] = (e == ENOENT || e == ENOTDIR || e == EBADF || e == ELOOP) ? 0 : -1;
+      }
+    });
+  } catch (...) {
+    return mrag::fail(MRAG_ERR_OOM, "paths: host allocation failed");
+  }
   return MRAG_OK;
 }
 

@@ -445,3 +445,19 @@ def test_batched_chunk_lookup_equals_per_hit(tmp_path):
         r._METADATA_STORE = old
     assert [c.model_dump() if c else None for c in batched] == [c.model_dump() if c else None for c in per_hit]
     assert batched[5] is None and batched[0] is not None
+
+
+def test_paths_exist_equals_pathlib(tmp_path):
+    """index_image_nodes' existence filter (one mrag_paths_exist call) gives Path(s).exists() for
+    every kind of path the reference's per-node check sees."""
+    from pathlib import Path
+
+    from app.ml.index_build import _paths_exist
+
+    f = tmp_path / "a.png"
+    f.write_bytes(b"x")
+    (tmp_path / "d").mkdir()
+    (tmp_path / "loop").symlink_to(tmp_path / "loop")
+    cases = [str(f), str(tmp_path / "missing.png"), "", ".", str(tmp_path / "d"), str(f) + "/x",
+             str(tmp_path) + "//a.png", "a\0b", str(tmp_path / "loop"), str(tmp_path / "d" / ".." / "a.png")]
+    assert _paths_exist(cases) == [Path(s).exists() for s in cases]
