@@ -283,6 +283,12 @@ int mrag_paths_exist(const char* const* paths, int32_t n, int32_t threads, int32
  * 3 f32 C += , 4 f32 out). N % 128 == 0, K % 64 == 0; bias and C 16-byte aligned. */
 int mrag_gemm_nt(const void* A, const void* W, const float* bias, void* C, int32_t M, int32_t N, int32_t K,
                  int32_t epilogue, void* stream);
+/* The same with the kernel chosen: 0 the automatic rule, 1 K3 (128 x 128 tiles), 2 K3d (persistent
+ * 256 x 256), 3 K3s (M <= 64), 4 K3w (weight-stationary: f16 epilogues, K 384 / 512, N % 192 == 0 or
+ * N % 256 == 0, M >= 4096). Every kernel gives the same bytes (one accumulation order); this entry
+ * exists for per-kernel timing and the bit-identity tests. */
+int mrag_gemm_nt_kernel(const void* A, const void* W, const float* bias, void* C, int32_t M, int32_t N, int32_t K,
+                        int32_t epilogue, int32_t kernel, void* stream);
 
 
 #ifdef __cplusplus

@@ -46,10 +46,16 @@ def _register_signatures():
         "mrag_encoder_embed_images": [vp, vp, i32, vp, i32, i32, vp],
         "mrag_encoder_embed_tokens": [vp, vp, vp, i32, i32, vp, i32, i32, vp],
         "mrag_gemm_nt": [vp, vp, vp, vp, i32, i32, i32, i32, vp],
+        "mrag_gemm_nt_kernel": [vp, vp, vp, vp, i32, i32, i32, i32, i32, vp],
         "mrag_encoder_score_pairs": [vp, vp, vp, vp, i32, i32, vp, i32, vp],
     }
     for name, args in sigs.items():
-        fn = getattr(lib, name)
+        try:
+            fn = getattr(lib, name)
+        except AttributeError:
+            if name == "mrag_gemm_nt_kernel":  # timing / test entry, absent from older builds (A/B)
+                continue
+            raise
         fn.restype = ctypes.c_int32
         fn.argtypes = args
     return lib
@@ -171,16 +177,25 @@ class GpuEncoder:
         return out
 
 
-def gemm_nt(A, W, bias, C, epilogue: int):
-    """K3 GEMM on torch CUDA tensors (test / building-block entry)."""
+GEMM_KERNELS = {"auto": 0, "k3": 1, "k3d": 2, "k3s": 3, "k3w": 4}
+
+
+def gemm_nt(A, W, bias, C, epilogue: int, kernel: str = "auto"):
+    """The encoder GEMM on torch CUDA tensors (test / building-block entry): the automatic kernel
+    choice of the towers, or one kernel forced (``GEMM_KERNELS``: bit-identity tests, timing)."""
     import torch
 
     lib = _register_signatures()
     M, K = A.shape
     N = W.shape[0]
     stream = torch.cuda.current_stream(A.device).cuda_stream
-    _native.check(lib.mrag_gemm_nt(A.data_ptr(), W.data_ptr(), bias.data_ptr() if bias is not None else None,
-                                   C.data_ptr(), M, N, K, epilogue, stream), "mrag_gemm_nt")
+    bp = bias.data_ptr() if bias is not None else None
+    if kernel == "auto":
+        _native.check(lib.mrag_gemm_nt(A.data_ptr(), W.data_ptr(), bp, C.data_ptr(), M, N, K, epilogue, stream),
+                      "mrag_gemm_nt")
+    else:
+        _native.check(lib.mrag_gemm_nt_kernel(A.data_ptr(), W.data_ptr(), bp, C.data_ptr(), M, N, K, epilogue,
+                                              GEMM_KERNELS[kernel], stream), "mrag_gemm_nt_kernel")
     return C
 
 

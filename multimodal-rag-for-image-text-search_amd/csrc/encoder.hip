@@ -933,4 +933,23 @@ int mrag_gemm_nt(const void* A, const void* W, const float* bias, void* C, int32
   return gemm(A, W, bias, C, M, N, K, N, epilogue, (hipStream_t)stream);
 }
 
+int mrag_gemm_nt_kernel(const void* A, const void* W, const float* bias, void* C, int32_t M, int32_t N, int32_t K,
+                        int32_t epilogue, int32_t kernel, void* stream) {
+  MRAG_REQUIRE(A && W && C, "NULL pointer");
+  MRAG_REQUIRE(M >= 0 && N > 0 && K > 0, "bad shape");
+  MRAG_REQUIRE(kernel >= GEMM_AUTO && kernel <= GEMM_K3W, "bad kernel %d", kernel);
+  GemmArgs g{};
+  g.A = (const _Float16*)A;
+  g.W = (const _Float16*)W;
+  g.bias = bias;
+  g.C = C;
+  g.M = M;
+  g.N = N;
+  g.K = K;
+  g.lda = K;
+  g.ldw = K;
+  g.ldc = N;
+  return launch_gemm(g, epilogue, (hipStream_t)stream, kernel);
+}
+
 }  // extern "C"

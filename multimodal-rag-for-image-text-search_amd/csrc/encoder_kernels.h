@@ -40,7 +40,10 @@ struct AttentionArgs {
   float scale;
 };
 
-int launch_gemm(const GemmArgs& g, int epi, hipStream_t s);
+// kernel: GEMM_AUTO (the rule in launch_gemm) or one kernel forced (A/B timing, bit-identity tests)
+enum GemmKernel { GEMM_AUTO = 0, GEMM_K3 = 1, GEMM_K3D = 2, GEMM_K3S = 3, GEMM_K3W = 4 };
+int launch_gemm(const GemmArgs& g, int epi, hipStream_t s, int kernel = GEMM_AUTO);
+bool gemm_ws_fits(const GemmArgs& g, int epi);
 int launch_layernorm(const LayerNormArgs& a, hipStream_t s);
 int launch_attention(const AttentionArgs& a, int dh, hipStream_t s);
 int launch_vit_im2col(const uint8_t* img, _Float16* out, int B, int S, int P, hipStream_t s);

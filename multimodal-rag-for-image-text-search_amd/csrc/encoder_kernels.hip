@@ -751,6 +751,230 @@ __global__ __launch_bounds__(G8_THREADS) void gemm_8p_kernel(GemmArgs g) {
 }
 
 // ---------------------------------------------------------------------------
+// K3w (weight-stationary; the text towers' K <= 512 GEMMs with an f16 epilogue: q|k|v and fc1 of
+// MiniLM-L6 and CLIP text at the config-5 batch, M = 16,000). The MLP / attention projections of
+// modeling_bert.py:282-350 and modeling_clip.py:293-296,343-350 with K = 384 or 512 are too short
+// for K3d's k-loop (six or eight 64-deep k-tiles per 256 x 256 tile: its fill and the epilogue set
+// the time, 0.16-0.29 of the MFMA peak). Here a wave keeps its 16 NB weight columns over the
+// whole K in the accumulator file for the whole launch (NB = 4, K = 512: 256 AGPRs), as K7 keeps
+// its queries, and the activation rows stream through LDS in 64-row tiles by LDS-DMA, double
+// buffered, one barrier per tile: per 32-deep k-step 4 NB MFMA 16x16x32 (the weight fragment as
+// operand A, the activation fragment as operand B, one accumulator per output block, ascending k:
+// K3's element order and K3's gemm_store4 epilogue, so rows are bit-identical to K3 / K3d). The
+// previous tile's epilogue (bias, activation, f16 store) and the next tile's LDS-DMA pieces run
+// in the MFMA gaps of the tile's first k-steps. Block b: panel p of 4 x 16 NB columns, row range
+// r (tiles r, r + R, ...); where R % 8 == 0 the P panels of a row range share an XCD (blocks
+// b = 8 s + x, s = r / 8 * P + p: an activation tile is fetched into one L2; speed only).
+constexpr int WS_ROWS = 64, WS_WAVES = 4, WS_THREADS = 64 * WS_WAVES;
+
+__device__ __forceinline__ void ws_mfma(f32x4& acc, const half8& w, const half8& a) {
+  asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+v"(acc) : "a"(w), "v"(a));
+}
+__device__ __forceinline__ void ws_mfma0(f32x4& acc, const half8& w, const half8& a) {
+  asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, 0" : "=&v"(acc) : "a"(w), "v"(a));
+}
+
+template <int EPI, int NB, int KT>
+__global__ __launch_bounds__(WS_THREADS) void gemm_ws_kernel(GemmArgs g, int P, int R, int xcd_map) {
+  constexpr int K = 32 * KT, ROW_BYTES = 2 * K, CPR = K / 8, TILE_BYTES = WS_ROWS * ROW_BYTES;
+  constexpr int PW = TILE_BYTES / 1024 / WS_WAVES;  // 1 KiB LDS-DMA pieces per wave per tile
+  constexpr int FRONT = 4;                          // pieces per k-step (k-steps 0 .. PW / 4 - 1)
+  constexpr int NA = 5;                             // A-fragment ring
+  constexpr int NFR = 4 * KT;                       // A fragments per tile: (kk, rb)
+  constexpr int NBLK = 4 * NB;                      // output blocks per wave per tile
+  constexpr int KDMA = PW / FRONT;                   // k-steps that issue the next tile's pieces
+  constexpr int NST = 8;                             // output stores per wave per tile (8 rows each)
+  constexpr int OUT_OFF = 2 * TILE_BYTES, OUT_WAVE = WS_ROWS * 128;  // per-wave 64 x 128-B output image
+  static_assert(CPR % 16 == 0 && PW % FRONT == 0, "tile geometry");
+  constexpr int KD0 = 3;                             // first k-step of the DMA pieces
+  constexpr int WSLOTS = 4 * (KT - 2);               // output-block write slots: k-steps 2 .. KT - 1
+  static_assert(NB >= 2 && NB <= 4 && KD0 + KDMA <= KT && NBLK <= WSLOTS, "slot plan");
+  __shared__ __attribute__((aligned(16))) char smem[2 * TILE_BYTES + WS_WAVES * OUT_WAVE];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int c16 = lane & 15, g4 = lane >> 4;
+  const uint32_t lds_base = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)((AS3 char*)smem));
+
+  int p, r;
+  if (xcd_map) {
+    const int s = (int)blockIdx.x >> 3;
+    p = s % P;
+    r = (s / P) * 8 + ((int)blockIdx.x & 7);
+  } else {
+    p = (int)blockIdx.x % P;
+    r = (int)blockIdx.x / P;
+  }
+  const int mtiles = (g.M + WS_ROWS - 1) / WS_ROWS;
+  const int my_tiles = r < mtiles ? (mtiles - 1 - r) / R + 1 : 0;
+  if (my_tiles <= 0) return;  // whole workgroup, before any barrier
+  const int n0 = (p * WS_WAVES + w) * 16 * NB;
+
+  // LDS image of a tile: row j, 16-byte chunk c at position c ^ (j & 15) (conflict-free fragment
+  // reads); piece (w PW + i) of a tile = 64 consecutive chunks of the image, one per lane
+  auto stage_piece = [&](int buf, int tile, int i) {
+    const int piece = w * PW + i;
+    const int q = piece * 64 + lane;
+    const int row = q / CPR, pos = q - row * CPR;
+    const int c = pos ^ (row & 15);
+    const int m = min(tile * WS_ROWS + row, g.M - 1);
+    glds_x4(g.A + (size_t)m * g.lda + c * 8, lds_base + (uint32_t)(buf * TILE_BYTES + piece * 1024));
+  };
+  // the first tile's pieces go out before the weight loads, so the two overlap
+#pragma unroll
+  for (int i = 0; i < PW; ++i) stage_piece(0, r, i);
+
+  // this wave's weight columns n0 + 16 cb + c16, all of K, in AGPRs for the launch
+  half8 wf[KT][NB];
+#pragma unroll
+  for (int kk = 0; kk < KT; ++kk)
+#pragma unroll
+    for (int cb = 0; cb < NB; ++cb)
+      wf[kk][cb] = *(const half8*)(g.W + (size_t)(n0 + 16 * cb + c16) * g.ldw + 32 * kk + 8 * g4);
+#pragma unroll
+  for (int kk = 0; kk < KT; ++kk)
+#pragma unroll
+    for (int cb = 0; cb < NB; ++cb) asm volatile("" ::"a"(wf[kk][cb]));
+  float bias[NB][4];
+#pragma unroll
+  for (int cb = 0; cb < NB; ++cb) {
+    const f32x4 b4 = g.bias ? *(const f32x4*)(g.bias + n0 + 16 * cb + 4 * g4) : f32x4{};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) bias[cb][q] = b4[q];
+  }
+
+  // A fragment (kk, rb): row 16 rb + c16, chunk 4 kk + g4 -> position (4 kk + g4) ^ c16
+  const int offA0 = c16 * ROW_BYTES + 16 * (g4 ^ c16);
+  half8 a[NA];
+  auto read_a = [&](const char* tb, int n) {
+    const int kk = n >> 2, rb = n & 3;
+    a[n % NA] = *(const half8*)(tb + ((offA0 ^ ((kk & 3) << 6)) + (kk >> 2) * 256 + rb * 16 * ROW_BYTES));
+  };
+
+  f32x4 acc[2][4][NB];
+  int m0_1 = 0, m0_2 = 0;  // first rows of tiles it - 1 (blocks written now) and it - 2 (rows stored now)
+  // Epilogue through this wave's LDS output image (64 rows x 128 B; 8-byte unit u of row j at
+  // u ^ 2 (j & 7)): a block's four finished outputs (gemm_act of acc + bias: gemm_store4's
+  // arithmetic) as one ds_write_b64, then whole 128-byte rows out by 16-byte global stores — one
+  // store instruction = 8 rows x 128 B, 8 per tile, instead of 16 scattered 8-byte ones. During
+  // tile it: k-steps 0-2 store tile it - 2's image (each row read a k-step before its store), the
+  // next tile's pieces go out in k-steps 3 ..., and tile it - 1's blocks enter the image one per
+  // few k-steps from k-step 2 on (its VALU spread over the MFMA gaps, not in one burst).
+  char* const ow = smem + OUT_OFF + w * OUT_WAVE;
+  auto epi_write = [&](auto y_c, int e) {
+    constexpr int Y = decltype(y_c)::value;
+    typedef _Float16 half4 __attribute__((ext_vector_type(4)));
+    const int rb = e / NB, cb = e - (e / NB) * NB;
+    const int j = 16 * rb + c16, u = 4 * cb + g4;
+    const f32x4 v = acc[Y][rb][cb];
+    half4 h;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) h[q] = (_Float16)gemm_act<EPI>(v[q] + bias[cb][q]);
+    *(half4*)(ow + j * 128 + 8 * (u ^ (2 * (j & 7)))) = h;
+  };
+  // rows 8 s .. 8 s + 7 of the image are read one k-step before their store (a read right before
+  // its store made the wave wait for every LDS read in flight, the A-fragment ring included)
+  half8 orow[4];
+  auto epi_read = [&](int s) {
+    const int j = 8 * s + (lane >> 3), q = lane & 7;
+    orow[s & 3] = *(const half8*)(ow + j * 128 + 16 * (q ^ (j & 7)));
+  };
+  auto epi_store = [&](int s, int m0) {
+    const int j = 8 * s + (lane >> 3), q = lane & 7;
+    const int m = m0 + j;
+    if (m < g.M && q < 2 * NB) *(half8*)((_Float16*)g.C + (size_t)m * g.ldc + n0 + 8 * q) = orow[s & 3];
+  };
+
+  auto tile_body = [&](auto x_c, int it) {
+    constexpr int X = decltype(x_c)::value;
+    constexpr int Y = 1 - X;
+    const int tile = r + it * R;
+    const bool has_next = it + 1 < my_tiles;
+    const bool has_prev = it > 0, has_prev2 = it > 1;
+    const char* tb = smem + X * TILE_BYTES;
+#pragma unroll
+    for (int n = 0; n < NA; ++n) read_a(tb, n);
+    mrag::static_for<KT>([&](auto kk_c) {
+      constexpr int kk = decltype(kk_c)::value;
+      mrag::static_for<4 * NB>([&](auto j_c) {
+        constexpr int j = decltype(j_c)::value;
+        constexpr int rb = j / NB, cb = j % NB;
+        constexpr int n = 4 * kk + rb;
+        if constexpr (kk == 0)
+          ws_mfma0(acc[X][rb][cb], wf[kk][cb], a[n % NA]);
+        else
+          ws_mfma(acc[X][rb][cb], wf[kk][cb], a[n % NA]);
+        if constexpr (cb == NB - 1) {  // fragment n's last MFMA issued: read fragment n + NA
+          if constexpr (n + NA < NFR) read_a(tb, n + NA);
+        } else if constexpr (cb == 0) {  // tile it - 2's rows out, or the next tile's piece
+          if constexpr (kk == 0) {
+            if (has_prev2) epi_read(rb);
+          } else if constexpr (kk == 1) {
+            if (has_prev2) {
+              epi_store(rb, m0_2);
+              epi_read(4 + rb);
+            }
+          } else if constexpr (kk == 2) {
+            if (has_prev2) epi_store(4 + rb, m0_2);
+          } else if constexpr (kk >= KD0 && FRONT * (kk - KD0) + rb < PW) {
+            if (has_next) stage_piece(Y, tile + R, FRONT * (kk - KD0) + rb);
+          }
+        } else if constexpr (cb == 1) {  // tile it - 1's output block e -> LDS (slot s = e WSLOTS / NBLK)
+          if constexpr (kk >= 2) {
+            constexpr int s = 4 * (kk - 2) + rb;
+            constexpr int e = (s * NBLK + WSLOTS - 1) / WSLOTS;
+            if constexpr (e < NBLK && e * WSLOTS / NBLK == s) {
+              if (has_prev) epi_write(std::integral_constant<int, Y>{}, e);
+            }
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      });
+    });
+    // the stores went out in k-steps 1-2, before the pieces (k-steps 3 ...): this lands both
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    m0_2 = m0_1;
+    m0_1 = tile * WS_ROWS;
+    __syncthreads();
+  };
+
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the first tile and the weights
+  __syncthreads();
+  for (int it = 0; it < my_tiles; it += 2) {
+    tile_body(std::integral_constant<int, 0>{}, it);
+    if (it + 1 < my_tiles) tile_body(std::integral_constant<int, 1>{}, it + 1);
+  }
+  // the image holds the second-to-last tile's rows (written during the last tile): out with them
+  if (my_tiles > 1) {
+#pragma unroll
+    for (int s = 0; s < NST; ++s) {
+      epi_read(s);
+      epi_store(s, m0_2);
+    }
+  }
+  // the last tile's blocks: its MFMAs were the last instructions issued, so wait out their
+  // results (MFMA -> VALU distance; the compiler does not see through the inline asm)
+  asm volatile("s_nop 15\n\ts_nop 7" ::: "memory");
+  if (my_tiles & 1) {
+#pragma unroll
+    for (int e = 0; e < NBLK; ++e) {
+      asm volatile("" : "+v"(acc[0][e / NB][e % NB]));
+      epi_write(std::integral_constant<int, 0>{}, e);
+    }
+  } else {
+#pragma unroll
+    for (int e = 0; e < NBLK; ++e) {
+      asm volatile("" : "+v"(acc[1][e / NB][e % NB]));
+      epi_write(std::integral_constant<int, 1>{}, e);
+    }
+  }
+#pragma unroll
+  for (int s = 0; s < NST; ++s) {
+    epi_read(s);
+    epi_store(s, m0_1);
+  }
+}
+
+// ---------------------------------------------------------------------------
 // K2: LayerNorm over rows of D <= 1024 (one wave per row, two-pass mean/var in f32).
 // Optional row gather (pooling), f32 and/or f16 outputs (in-place f32 allowed).
 __global__ __launch_bounds__(256) void layernorm_kernel(LayerNormArgs a) {
@@ -950,6 +1174,24 @@ __device__ __forceinline__ half4_t lds_read_tr16(const _Float16* p) {
   return __builtin_bit_cast(half4_t, v);
 }
 
+// V image of a key block in LDS: row r (key) of DH halves, no padding, 16-byte chunk j stored at
+// position j ^ v_swz(r). Bank-conflict free for both accesses (MI355X_MICROARCH.md LDS table):
+// the staging ds_write_b128 (8 contiguous lanes = whole rows: a permutation of each row's chunks),
+// and the transposed ds_read_b64_tr_b16 of O^T += V^T P^T, whose 32-lane group reads 8 rows x 2
+// chunks — the swizzle spreads those 16 chunks over the 16 four-bank slots (DH = 64: rows r and
+// r + 1 share a slot base, so r & 6 moves the chunk pair; DH = 32: rows r and r + 4 share one,
+// so (r >> 1) & 2 does). The padded row strides of round 5 left 2-way conflicts on the reads
+// (DH = 64) or on the writes (DH = 32).
+template <int DH>
+__device__ __forceinline__ int v_swz(int r) {
+  return DH == 64 ? (r & 6) : ((r >> 1) & 2);
+}
+// half offset of (row r, half column col) in such an image (col within one chunk's 8 halves kept)
+template <int DH>
+__device__ __forceinline__ int v_off(int r, int col) {
+  return r * DH + ((((col >> 3) ^ v_swz<DH>(r)) << 3) | (col & 7));
+}
+
 // K4 v3 (flash form, any L <= 512, head_dim 32 or 64): one wave per (sequence, head, 16-query
 // block); key blocks of 16 with an online softmax, all on MFMA 16x16:
 //   S^T = K . Q^T    (16x16x32, DH/32 k-steps): lane (c, g) = (l & 15, l >> 4) holds query
@@ -967,9 +1209,8 @@ template <int DH>
 __global__ __launch_bounds__(256) void attention_flash16_kernel(AttentionArgs a) {
   constexpr int KS = DH / 32;               // 32-dim k-steps of S^T
   constexpr int DB = DH / 16;               // 16-dim blocks of O^T
-  constexpr int VROW = DH == 64 ? 96 : 48;  // LDS row stride (halves): a transposed read's 4 rows hit disjoint banks
   typedef _Float16 half4_v __attribute__((ext_vector_type(4)));
-  __shared__ __attribute__((aligned(16))) _Float16 Vs[4][16 * VROW];
+  __shared__ __attribute__((aligned(16))) _Float16 Vs[4][16 * DH];  // v_off layout
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int c = lane & 15, g = lane >> 4;
   const int L = a.L, nqb = (L + 15) >> 4;
@@ -1033,7 +1274,7 @@ __global__ __launch_bounds__(256) void attention_flash16_kernel(AttentionArgs a)
 #pragma unroll
     for (int t = 0; t < KS; ++t) {
       const int idx = lane + 64 * t, key = idx / (DH / 8), ch = idx % (DH / 8);
-      *(half8*)(vs + key * VROW + 8 * ch) = cur.vv[t];
+      *(half8*)(vs + v_off<DH>(key, 8 * ch)) = cur.vv[t];
     }
     float sv[4], bmax = -INFINITY;
 #pragma unroll
@@ -1060,7 +1301,7 @@ __global__ __launch_bounds__(256) void attention_flash16_kernel(AttentionArgs a)
 #pragma unroll
     for (int db = 0; db < DB; ++db) {
       o[db] *= alpha;
-      const half4_t vt = lds_read_tr16(vs + (4 * g + (c >> 2)) * VROW + 16 * db + 4 * (c & 3));
+      const half4_t vt = lds_read_tr16(vs + v_off<DH>(4 * g + (c >> 2), 16 * db + 4 * (c & 3)));
       o[db] = __builtin_amdgcn_mfma_f32_16x16x16f16(vt, pf, o[db], 0, 0, 0);
     }
   }
@@ -1091,11 +1332,12 @@ __global__ __launch_bounds__(256) void attention_flash16_kernel(AttentionArgs a)
 template <int DH>
 __global__ __launch_bounds__(256) void attention_seq64_kernel(AttentionArgs a) {
   constexpr int KS = DH / 32, DB = DH / 16;
-  constexpr int VROW = DH == 64 ? 96 : 48;  // as attention_flash16_kernel
-  constexpr int KROW = DH + 8;              // K image row stride (halves): 16-B reads of 16 rows spread banks
   typedef _Float16 half4_v __attribute__((ext_vector_type(4)));
-  __shared__ __attribute__((aligned(16))) _Float16 Ks[64 * KROW];
-  __shared__ __attribute__((aligned(16))) _Float16 Vs[64 * VROW];
+  // K image: rows of DH halves, 16-byte chunk j at j ^ ((r >> 1) & (DH / 8 - 1)) — the K-fragment
+  // ds_read_b128 of 16 rows x one chunk column per lane quarter covers all 64 banks (the GEMMs'
+  // swz_off rule); V image: v_off (as attention_flash16_kernel)
+  __shared__ __attribute__((aligned(16))) _Float16 Ks[64 * DH];
+  __shared__ __attribute__((aligned(16))) _Float16 Vs[64 * DH];
   __shared__ int kok[64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int c = lane & 15, g = lane >> 4;
@@ -1129,11 +1371,12 @@ __global__ __launch_bounds__(256) void attention_seq64_kernel(AttentionArgs a) {
     const int key = threadIdx.x;
     ok = key < L && (!a.mask || a.mask[(size_t)b * L + key] != 0);
   }
+  auto k_off = [&](int r, int ch) { return r * DH + 8 * (ch ^ ((r >> 1) & (CH - 1))); };
 #pragma unroll
   for (int t = 0; t < NST; ++t) {
     const int idx = threadIdx.x + 256 * t, key = idx / CH, ch = idx % CH;
-    *(half8*)(Ks + key * KROW + 8 * ch) = key < L ? kv[t] : half8{};
-    *(half8*)(Vs + key * VROW + 8 * ch) = key < L ? vv[t] : half8{};
+    *(half8*)(Ks + k_off(key, ch)) = key < L ? kv[t] : half8{};
+    *(half8*)(Vs + v_off<DH>(key, 8 * ch)) = key < L ? vv[t] : half8{};
   }
   if (threadIdx.x < 64) kok[threadIdx.x] = ok;
   if (qrow >= L) {
@@ -1159,7 +1402,7 @@ __global__ __launch_bounds__(256) void attention_seq64_kernel(AttentionArgs a) {
     f32x4 sacc = {};
 #pragma unroll
     for (int st = 0; st < KS; ++st) {
-      const half8 kf = *(const half8*)(Ks + (16 * kb + c) * KROW + 32 * st + 8 * g);
+      const half8 kf = *(const half8*)(Ks + k_off(16 * kb + c, 4 * st + g));
       sacc = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf, qf[st], sacc, 0, 0, 0);
     }
     float sv[4], bmax = -INFINITY;
@@ -1184,11 +1427,10 @@ __global__ __launch_bounds__(256) void attention_seq64_kernel(AttentionArgs a) {
     ps += __shfl_xor(ps, 32);
     l = l * alpha + ps;
     m = mn;
-    const _Float16* vs = Vs + 16 * kb * VROW;
 #pragma unroll
     for (int db = 0; db < DB; ++db) {
       o[db] *= alpha;
-      const half4_t vt = lds_read_tr16(vs + (4 * g + (c >> 2)) * VROW + 16 * db + 4 * (c & 3));
+      const half4_t vt = lds_read_tr16(Vs + v_off<DH>(16 * kb + 4 * g + (c >> 2), 16 * db + 4 * (c & 3)));
       o[db] = __builtin_amdgcn_mfma_f32_16x16x16f16(vt, pf, o[db], 0, 0, 0);
     }
   }
@@ -1394,18 +1636,75 @@ struct K3sKern {
   };
 };
 
-int launch_gemm(const GemmArgs& g, int epi, hipStream_t s) {
+// K3w's shapes: an f16 epilogue, K = 384 or 512 (the weight columns of a wave fit the accumulator
+// file), N a multiple of 256 (NB = 4) or 192 (NB = 3), enough rows for every CU
+bool gemm_ws_fits(const GemmArgs& g, int epi) {
+  const bool f16 = epi == EPI_F16 || epi == EPI_F16_QUICK_GELU || epi == EPI_F16_GELU_ERF;
+  return f16 && (g.K == 384 || g.K == 512) && (g.N % 256 == 0 || g.N % 192 == 0) && g.M >= 4096;
+}
+// The automatic rule takes K3w wherever it fits. Alone, per GEMM (profiles/r6s7_probe.jsonl,
+// M = 16,000): CLIP-text q|k|v 37.6 us against 41.6 on K3d, MiniLM q|k|v 26.9 against 31.7 on K3,
+// CLIP-text fc1 47.5 against 47.5 on K3d, MiniLM fc1 (erf) 42.2 against 46.3 on K3d (38.0 on K3);
+// in the config-5 leg, four steps in flight, two interleaved rounds on one box
+// (profiles/r6s9_fusion_ab.jsonl): 249.6k / 250.4k q/s against 248.6k / 248.4k with K3w on the
+// q|k|v GEMMs only and 241.0k / 246.7k before K3w.
+bool gemm_ws_auto(const GemmArgs& g, int epi) { return gemm_ws_fits(g, epi); }
+
+template <int NB, int KT>
+int launch_ws(const GemmArgs& g, int epi, hipStream_t s) {
+  const int P = g.N / (64 * NB);
+  const int cus = std::max(8, num_cus());
+  int R = std::max(1, cus / P);
+  int xcd_map = 0;
+  if (R >= 8 && (R / 8 * 8) * 10 >= R * 9) {  // an XCD-aligned row split costing <= 10 % of the CUs
+    R = R / 8 * 8;
+    xcd_map = 1;
+  }
+  const dim3 grid((unsigned)(P * R)), block(WS_THREADS);
+  switch (epi) {
+    case EPI_F16: hipLaunchKernelGGL((gemm_ws_kernel<EPI_F16, NB, KT>), grid, block, 0, s, g, P, R, xcd_map); break;
+    case EPI_F16_QUICK_GELU:
+      hipLaunchKernelGGL((gemm_ws_kernel<EPI_F16_QUICK_GELU, NB, KT>), grid, block, 0, s, g, P, R, xcd_map);
+      break;
+    case EPI_F16_GELU_ERF:
+      hipLaunchKernelGGL((gemm_ws_kernel<EPI_F16_GELU_ERF, NB, KT>), grid, block, 0, s, g, P, R, xcd_map);
+      break;
+    default: return mrag::fail(MRAG_ERR_ARG, "gemm K3w: epilogue %d unsupported", epi);
+  }
+  MRAG_CHECK_LAUNCH();
+  return MRAG_OK;
+}
+
+int launch_gemm_ws(const GemmArgs& g, int epi, hipStream_t s) {
+  MRAG_REQUIRE(gemm_ws_fits(g, epi), "gemm K3w: shape M=%d N=%d K=%d epilogue %d unsupported", g.M, g.N, g.K, epi);
+  const bool nb4 = g.N % 256 == 0;
+  if (g.K == 512) return nb4 ? launch_ws<4, 16>(g, epi, s) : launch_ws<3, 16>(g, epi, s);
+  return nb4 ? launch_ws<4, 12>(g, epi, s) : launch_ws<3, 12>(g, epi, s);
+}
+
+int launch_gemm(const GemmArgs& g, int epi, hipStream_t s, int kernel) {
   if (g.M <= 0) return MRAG_OK;
   MRAG_REQUIRE(g.N % GN == 0 && g.K % GK == 0, "gemm: N=%d must be a multiple of %d and K=%d of %d", g.N, GN, g.K,
                GK);
   MRAG_REQUIRE(g.lda % 8 == 0 && g.ldw % 8 == 0 && g.ldc % 4 == 0, "gemm: lda/ldw must be multiples of 8, ldc of 4");
   MRAG_REQUIRE(((uintptr_t)g.bias & 15) == 0 && ((uintptr_t)g.C & 15) == 0, "gemm: bias and C must be 16-byte aligned");
-  if (g.M >= 1024 && g.N <= G8_BIAS_MAX && g.N % 256 == 0 && !k3_beats_k3d(g)) {
+  if (kernel == GEMM_K3W || (kernel == GEMM_AUTO && gemm_ws_auto(g, epi))) return launch_gemm_ws(g, epi, s);
+  if (kernel == GEMM_K3D) {
+    MRAG_REQUIRE(g.M >= 1024 && g.N <= G8_BIAS_MAX && g.N % 256 == 0, "gemm K3d: shape M=%d N=%d unsupported", g.M,
+                 g.N);
     const int ntiles = ((g.M + G8Geom::BM - 1) / G8Geom::BM) * (g.N / G8Geom::BN);
     const int nb = std::min((ntiles + 7) / 8 * 8, std::max(8, num_cus() / 8 * 8));
     return launch_epi<K3dKern>(epi, dim3((unsigned)nb), dim3(G8_THREADS), s, g);
   }
-  if (g.M <= 64) {
+  if (kernel == GEMM_K3S) {
+    MRAG_REQUIRE(g.M <= 64, "gemm K3s: M=%d > 64", g.M);
+  }
+  if (kernel == GEMM_AUTO && g.M >= 1024 && g.N <= G8_BIAS_MAX && g.N % 256 == 0 && !k3_beats_k3d(g)) {
+    const int ntiles = ((g.M + G8Geom::BM - 1) / G8Geom::BM) * (g.N / G8Geom::BN);
+    const int nb = std::min((ntiles + 7) / 8 * 8, std::max(8, num_cus() / 8 * 8));
+    return launch_epi<K3dKern>(epi, dim3((unsigned)nb), dim3(G8_THREADS), s, g);
+  }
+  if ((kernel == GEMM_AUTO && g.M <= 64) || kernel == GEMM_K3S) {
     const dim3 grid((unsigned)(g.N / 16));
     switch ((g.M + 15) / 16) {
       case 1: return launch_epi<K3sKern<1>::Kern>(epi, grid, dim3(64), s, g);

@@ -35,6 +35,7 @@ ap.add_argument("--sets", type=int, default=3, help="activation / output buffer 
 ap.add_argument("--operands", choices=["randn", "small", "zeros"], default="randn",
                 help="activation values: N(0,1), N(0,1) x 1e-3, or zeros (switching activity A/B)")
 ap.add_argument("--only", default="", help="comma-separated tower:gemm names")
+ap.add_argument("--epi", type=int, default=-1, help="override every shape's epilogue (A/B of the epilogue cost)")
 args = ap.parse_args()
 if args.only:
     keep = set(args.only.split(","))
@@ -45,6 +46,8 @@ lib.mrag_gemm_nt.restype = ctypes.c_int
 dev = torch.device("cuda", 0)
 g = torch.Generator(device=dev).manual_seed(0)
 for tower, name, M, N, K, epi in SHAPES:
+    if args.epi >= 0:
+        epi = args.epi
     W = (torch.randn(N, K, device=dev, generator=g) * 0.02).half()
     bias = torch.randn(N, device=dev, generator=g) * 0.01
     sets = []

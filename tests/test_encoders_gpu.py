@@ -276,6 +276,39 @@ def test_gemm_skinny_rows_equal_k3(cuda, N, K):
             assert err < (2e-3 if epi <= 2 else 2e-5), (M, N, K, epi, err)
 
 
+@pytest.mark.parametrize("N,K", [(1536, 512), (2048, 512), (1152, 384), (1536, 384), (768, 512), (384, 384)])
+def test_gemm_weight_stationary_equals_k3(cuda, N, K):
+    """K3w (the weight-stationary kernel the text towers' q|k|v and fc1 take at K 384 / 512) against
+    K3 forced on the same operands: bit-identical for the three f16 epilogues (one accumulation
+    order, K3's epilogue), with M a multiple of the 64-row tile, ragged (the last tile partly past
+    M: clamped loads, no stores), and small enough that some row ranges own no tile or one tile;
+    and within K3's tolerance of a torch fp32 product. The automatic rule takes K3w for these
+    shapes at M >= 4096."""
+    import torch
+
+    from app.encoders import gemm_nt
+
+    g = torch.Generator(device=cuda).manual_seed(7 * N + K)
+    for M in (16000, 4100, 4096 + 63, 5000):
+        A = (torch.randn(M, K, generator=g, device=cuda) * 0.5).half()
+        W = (torch.randn(N, K, generator=g, device=cuda) * 0.05).half()
+        bias = torch.randn(N, generator=g, device=cuda) * 0.1
+        ref = A.float() @ W.float().t() + bias
+        for epi in range(3):
+            outs = {}
+            for kern in ("k3", "k3w", "auto"):
+                C = torch.full((M, N), float("nan"), dtype=torch.float16, device=cuda)
+                gemm_nt(A, W, bias, C, epi, kernel=kern)
+                outs[kern] = C
+            torch.cuda.synchronize()
+            assert not torch.isnan(outs["k3w"].float()).any(), (M, N, K, epi)
+            assert torch.equal(outs["k3w"], outs["k3"]), ("K3w != K3", M, N, K, epi)
+            assert torch.equal(outs["auto"], outs["k3"]), ("auto != K3", M, N, K, epi)  # whichever kernel auto picks
+            if epi == 0:
+                err = (outs["k3w"].float() - ref).abs().max().item() / ref.abs().max().item()
+                assert err < 2e-3, (M, N, K, err)
+
+
 def test_gelu_erf_epilogue_sweep(cuda):
     """the erf-GELU epilogue (A&S 7.1.26 + hardware rcp/exp2) swept over x in
     [-8, 8) against torch.nn.functional.gelu (exact erf) on the fp16 output, with an absolute
