@@ -165,6 +165,9 @@ def index_image_nodes(user_id: str, nodes: Sequence[Dict[str, object]]) -> List[
                              "source": metadata.get("source")})
             out.append(VectorRow(chunk_id=chunk_id, user_id=user_id, document_id=metadata["doc_id"], modality="image",
                                  embedding=[], meta=metadata))
+        if native:  # this package's store: the metadata JSON it writes, made here beside the embedding
+            for row in out:
+                row._meta_json = json.dumps(row.meta or {})
         return out
 
     if native and len(sel) >= 256:

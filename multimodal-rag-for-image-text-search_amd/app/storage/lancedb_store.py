@@ -214,11 +214,12 @@ class LanceDBStore:
 
     @staticmethod
     def _normalize_rows(vectors: np.ndarray) -> np.ndarray:
-        """``_normalize`` of every row of an f32 [n, dim] array at once, bit for bit: the same
-        np.linalg.norm per row (its dot product's summation order is BLAS's, so it is not batched),
-        then one f32 division of each row by its norm; rows of norm <= 0 stay as they are."""
+        """``_normalize`` of every row of an f32 [n, dim] array at once, bit for bit: np.linalg.norm
+        of a 1-D f32 vector is sqrt(x.dot(x)) — the same BLAS dot per row (its summation order is
+        BLAS's, so it is not batched) and an f32 sqrt of the result — then one f32 division of each
+        row by its norm; rows of norm <= 0 stay as they are."""
         arr = np.asarray(vectors, dtype=np.float32)
-        norms = np.array([np.linalg.norm(x) for x in arr], dtype=np.float32).reshape(-1, 1)
+        norms = np.sqrt(np.array([x.dot(x) for x in arr], dtype=np.float32)).reshape(-1, 1)
         out = arr / np.where(norms <= 0, np.float32(1), norms)
         return np.where(norms <= 0, arr, out)
 
@@ -235,7 +236,9 @@ class LanceDBStore:
                 "document_id": row.document_id,
                 "modality": row.modality,
                 "embedding": vectors[i],
-                "meta": json.dumps(row.meta or {}),
+                # index_image_nodes serialises the metadata on its helper thread while the images
+                # embed (index_build._meta_json); the same json.dumps otherwise
+                "meta": getattr(row, "_meta_json", None) or json.dumps(row.meta or {}),
             }
             for i, row in enumerate(rows)
         ]
