@@ -17,7 +17,7 @@ from __future__ import annotations
 
 import os
 from pathlib import Path
-from typing import Any, List, Mapping, Optional, Sequence
+from typing import Any, Mapping, Optional, Sequence
 
 import numpy as np
 
@@ -101,6 +101,22 @@ def embed_images_batch(paths: Sequence[Path], batch_size: int = 8) -> np.ndarray
     """Embed images with CLIP's vision tower and return normalised float32 rows."""
     if not paths:
         return np.empty((0, 512), dtype=np.float32)
+    return _normalize(np.vstack(list(_image_feature_batches(paths, batch_size))))
+
+
+def embed_images_batches(paths: Sequence[Path], batch_size: int = 8):
+    """``embed_images_batch`` one encoder batch at a time: yields the normalised rows of each
+    batch in order, while the next batches' files are read and decoded on the pipeline's threads
+    (index_image_nodes prepares the store's rows of batch i while batch i + 1 encodes). The rows
+    equal embed_images_batch's: ``_normalize`` reduces each row on its own."""
+    for raw in _image_feature_batches(paths, batch_size):
+        yield _normalize(raw)
+
+
+def _image_feature_batches(paths: Sequence[Path], batch_size: int):
+    """The vision tower's unnormalised features, one array per encoder batch."""
+    if not paths:
+        return
     from PIL import Image
 
     from app.encoders.models import ClipModel, ClipProcessor
@@ -110,7 +126,6 @@ def embed_images_batch(paths: Sequence[Path], batch_size: int = 8) -> np.ndarray
     native = isinstance(model, ClipModel) and isinstance(processor, ClipProcessor)
     step = max(batch_size, 256) if native else batch_size
     paths = list(paths)
-    out: List[np.ndarray] = []
     if native and os.environ.get("MRAG_HOST_RESIZE") != "1":
         # three stages in flight: the host prepares group g + 2 (file reads, probes, PNG inflate,
         # Pillow for what the GPU decoders do not take), a second thread decodes group g + 1 on the
@@ -153,9 +168,9 @@ def embed_images_batch(paths: Sequence[Path], batch_size: int = 8) -> np.ndarray
                 preps.pop(i, None)
                 for c0 in range(0, n_i, step):
                     inputs = processor.from_device(imgs, c0, step)
-                    out.append(_to_numpy(model.get_image_features(**_kwargs(inputs))))
+                    yield _to_numpy(model.get_image_features(**_kwargs(inputs)))
                 del imgs
-        return _normalize(np.vstack(out))
+        return
     for start in range(0, len(paths), step):
         batch_paths = paths[start:start + step]
         if native:
@@ -167,8 +182,7 @@ def embed_images_batch(paths: Sequence[Path], batch_size: int = 8) -> np.ndarray
                 img.close()
         if hasattr(inputs, "to"):
             inputs = inputs.to(_device())
-        out.append(_to_numpy(model.get_image_features(**_kwargs(inputs))))
-    return _normalize(np.vstack(out))
+        yield _to_numpy(model.get_image_features(**_kwargs(inputs)))
 
 
 def embed_query_for_images(query: str) -> np.ndarray:
@@ -184,4 +198,4 @@ def embed_query_for_images(query: str) -> np.ndarray:
     return _normalize(array)[0]
 
 
-__all__ = ["embed_text_batch", "embed_images_batch", "embed_query_for_images"]
+__all__ = ["embed_text_batch", "embed_images_batch", "embed_images_batches", "embed_query_for_images"]

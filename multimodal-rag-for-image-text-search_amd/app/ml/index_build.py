@@ -13,13 +13,14 @@ from __future__ import annotations
 
 import json
 import os
+import sys
 import threading
 from pathlib import Path
 from typing import Dict, List, Sequence
 
 import numpy as np
 
-from app.ml.embeddings import embed_images_batch, embed_query_for_images, embed_text_batch
+from app.ml.embeddings import embed_images_batch, embed_images_batches, embed_query_for_images, embed_text_batch
 from app.ml.splitter import Document, SentenceSplitter
 from app.settings import settings
 from app.storage.lancedb_store import LanceDBStore, VectorRow
@@ -114,30 +115,44 @@ def _paths_exist(strs: List[str]) -> List[bool]:
     from app.encoders.preprocess import decode_workers
 
     n = len(strs)
-    enc, ok = [], [True] * n
-    for i, s in enumerate(strs):
-        try:
-            b = os.fsencode(s)
-        except UnicodeError:
-            b = None
-        if b is None or b"\0" in b:  # Path.exists: ValueError -> False
-            ok[i] = False
-            b = b""
-        enc.append(b)
+    try:  # os.fsencode of every path at once (what it does on POSIX)
+        enc = [s.encode(_FS_ENCODING, "surrogateescape") for s in strs]
+        bad = [i for i, b in enumerate(enc) if b"\0" in b]
+    except UnicodeError:
+        enc, bad = [], []
+        for i, s in enumerate(strs):
+            try:
+                enc.append(os.fsencode(s))
+                if b"\0" in enc[-1]:
+                    bad.append(i)
+            except UnicodeError:
+                enc.append(b"")
+                bad.append(i)
+    for i in bad:  # Path.exists: ValueError -> False
+        enc[i] = b""
     out = np.zeros(n, np.int32)
     if n:
         names = (ctypes.c_char_p * n)(*enc)
         _native.call("mrag_paths_exist", ctypes.cast(names, ctypes.c_void_p), n, min(8, decode_workers()),
                      out.ctypes.data)
-    res = []
-    for i in range(n):
-        if not ok[i]:
-            res.append(False)
-        elif out[i] < 0:
-            res.append(Path(strs[i]).exists())  # raises what the reference's check raises
-        else:
-            res.append(bool(out[i]))
+    out[bad] = 0
+    res = (out > 0).tolist()
+    for i in np.flatnonzero(out < 0).tolist():
+        res[i] = Path(strs[i]).exists()  # raises what the reference's check raises
     return res
+
+
+_FS_ENCODING = sys.getfilesystemencoding()
+_ROW_BUILDER = None  # one helper thread, kept: starting a thread per call cost ~1-5 ms
+
+
+def _row_builder():
+    global _ROW_BUILDER
+    if _ROW_BUILDER is None:
+        from concurrent.futures import ThreadPoolExecutor
+
+        _ROW_BUILDER = ThreadPoolExecutor(max_workers=1, thread_name_prefix="mrag-rows")
+    return _ROW_BUILDER
 
 
 def index_image_nodes(user_id: str, nodes: Sequence[Dict[str, object]]) -> List[Dict[str, object]]:
@@ -170,20 +185,25 @@ def index_image_nodes(user_id: str, nodes: Sequence[Dict[str, object]]) -> List[
                 row._meta_json = json.dumps(row.meta or {})
         return out
 
-    if native and len(sel) >= 256:
-        from concurrent.futures import ThreadPoolExecutor
-
-        with ThreadPoolExecutor(max_workers=1) as ex:
-            fut = ex.submit(build_rows)
-            embeddings = embed(paths)
+    array_rows = _array_rows()
+    if native and array_rows and len(sel) >= 256:
+        # the rows on a helper thread, and the store's normalisation of each encoder batch while
+        # the next one embeds; one upsert at the end as the reference's (same rows, same bytes)
+        fut = _row_builder().submit(build_rows)
+        try:
+            parts = [(e, LanceDBStore._normalize_rows(e)) for e in embed_images_batches(paths)]
+        finally:
             rows = fut.result()
+        embeddings = np.vstack([e for e, _ in parts])
+        for row, embedding in zip(rows, embeddings):
+            row.embedding = embedding
+        _LANCEDB_STORE._upsert_image_normalized(rows, np.vstack([v for _, v in parts]))
     else:
         rows = build_rows()
         embeddings = embed(paths)
-    array_rows = _array_rows()
-    for row, embedding in zip(rows, embeddings):
-        row.embedding = _row_embedding(embedding, array_rows)
-    _LANCEDB_STORE.upsert_image_vectors(rows)
+        for row, embedding in zip(rows, embeddings):
+            row.embedding = _row_embedding(embedding, array_rows)
+        _LANCEDB_STORE.upsert_image_vectors(rows)
     _bump_version(user_id)
     return [{"chunk_id": row.chunk_id, "metadata": row.meta} for row in rows]
 

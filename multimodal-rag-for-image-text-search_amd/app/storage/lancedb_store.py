@@ -81,11 +81,16 @@ class _Table:
     def _append_rows(self, vectors: np.ndarray, user_ids, chunk_ids, metas, doc_ids) -> None:
         labs = np.asarray([self.labels.setdefault(u, len(self.labels)) for u in user_ids], dtype=np.int32)
         first = self.index.add(np.asarray(vectors), labs)
-        for i, cid in enumerate(chunk_ids):
-            self.chunk_ids.append(cid)
-            self.metas.append(metas[i])
-            self.doc_ids.append(doc_ids[i])
-            self.by_chunk.setdefault(cid, []).append(first + i)
+        self.chunk_ids.extend(chunk_ids)
+        self.metas.extend(metas)
+        self.doc_ids.extend(doc_ids)
+        by_chunk = self.by_chunk
+        for row, cid in enumerate(chunk_ids, first):
+            rows = by_chunk.get(cid)
+            if rows is None:
+                by_chunk[cid] = [row]
+            else:
+                rows.append(row)
 
     def _kill_rows(self, dead) -> None:
         dead = [int(r) for r in dead]
@@ -224,11 +229,13 @@ class LanceDBStore:
         return np.where(norms <= 0, arr, out)
 
     @staticmethod
-    def _prepare_rows_array(rows: List[VectorRow]):
+    def _prepare_rows_array(rows: List[VectorRow], vectors: Optional[np.ndarray] = None):
         """``_prepare_rows`` for rows whose embeddings are numpy rows (what index_text_nodes /
         index_image_nodes hand this store): the same payload dicts and vector bytes with the
-        vectors kept as one f32 array — no per-row list round trip (tolist, then asarray)."""
-        vectors = LanceDBStore._normalize_rows(np.stack([np.asarray(r.embedding, dtype=np.float32) for r in rows]))
+        vectors kept as one f32 array — no per-row list round trip (tolist, then asarray).
+        ``vectors``: ``_normalize_rows`` of the rows' embeddings when the caller already made it."""
+        if vectors is None:
+            vectors = LanceDBStore._normalize_rows(np.stack([np.asarray(r.embedding, dtype=np.float32) for r in rows]))
         payloads = [
             {
                 "chunk_id": row.chunk_id,
@@ -252,6 +259,13 @@ class LanceDBStore:
             table.upsert(payloads, vectors)
         else:
             table.upsert(self._prepare_rows(rows))
+
+    def _upsert_image_normalized(self, rows: List[VectorRow], vectors: np.ndarray) -> None:
+        """``upsert_image_vectors(rows)`` when ``vectors`` already holds ``_normalize_rows`` of the
+        rows' embeddings (index_image_nodes computes it batch by batch while the images embed)."""
+        if rows:
+            payloads, vectors = self._prepare_rows_array(rows, vectors)
+            self._image_table.upsert(payloads, vectors)
 
     def upsert_text_vectors(self, rows: Iterable[VectorRow]) -> None:
         self._upsert(self._text_table, rows)

@@ -374,3 +374,38 @@ def test_null_stream_device_inputs_ordered(cuda):
         ids.copy_(torch.from_numpy(ids_h).to(cuda) + (0 * acc[:16, :24]).to(torch.int32))
         out = enc.embed_tokens(ids, mask)
         assert np.array_equal(out.cpu().numpy(), ref)
+
+
+def test_index_image_nodes_batched_rows_equal_reference_form(cuda, tmp_path, monkeypatch):
+    """index_image_nodes over more than one encoder batch (600 files, 7 missing) takes the batched
+    form (the store's normalisation per encoder batch while the next embeds, the rows on a helper
+    thread): the committed vectors are bit-identical to the reference's per-row
+    LanceDBStore._normalize of embed_images_batch's rows, and ids / metadata JSON are the
+    reference's (app/ml/index_build.py:110-155, app/storage/lancedb_store.py:63-85)."""
+    import json
+
+    from app.ml import embeddings, index_build
+    from app.storage.lancedb_store import LanceDBStore
+
+    store = LanceDBStore(str(tmp_path / "db3"))
+    monkeypatch.setattr(index_build, "_LANCEDB_STORE", store)
+    monkeypatch.setattr(index_build, "_VERSION_FILE", tmp_path / "versions.json")
+    rng = np.random.default_rng(4)
+    nodes, present = [], []
+    for i in range(600):
+        p = tmp_path / f"f{i}.{'png' if i % 4 == 0 else 'jpg'}"
+        if i % 97 != 5:
+            Image.fromarray(rng.integers(0, 256, (40 + i % 23, 50 + i % 31, 3), dtype=np.uint8)).save(p)
+            present.append(i)
+        nodes.append({"id": f"n{i}", "metadata": {"file_path": str(p), "page": i}})
+    out = index_build.index_image_nodes("u1", nodes)
+    assert [o["chunk_id"] for o in out] == [f"n{i}" for i in present]
+    emb = embeddings.embed_images_batch([str(tmp_path / f"f{i}.{'png' if i % 4 == 0 else 'jpg'}") for i in present])
+    exp = np.asarray([store_normalize(v) for v in emb], np.float32)
+    segs = list(store._image_table.files.segments())
+    assert len(segs) == 1
+    assert np.array_equal(np.asarray(segs[0].vectors), exp)
+    assert segs[0].rows["chunk_id"] == [f"n{i}" for i in present]
+    metas = [{"file_path": str(tmp_path / f"f{i}.{'png' if i % 4 == 0 else 'jpg'}"), "page": i, "doc_id": f"n{i}",
+              "user_id": "u1", "modality": "image", "source": None} for i in present]
+    assert segs[0].rows["meta"] == [json.dumps(m) for m in metas]
