@@ -180,24 +180,33 @@ def index_image_nodes(user_id: str, nodes: Sequence[Dict[str, object]]) -> List[
                              "source": metadata.get("source")})
             out.append(VectorRow(chunk_id=chunk_id, user_id=user_id, document_id=metadata["doc_id"], modality="image",
                                  embedding=[], meta=metadata))
-        if native:  # this package's store: the metadata JSON it writes, made here beside the embedding
-            for row in out:
-                row._meta_json = json.dumps(row.meta or {})
         return out
 
     array_rows = _array_rows()
     if native and array_rows and len(sel) >= 256:
-        # the rows on a helper thread, and the store's normalisation of each encoder batch while
-        # the next one embeds; one upsert at the end as the reference's (same rows, same bytes)
-        fut = _row_builder().submit(build_rows)
+        # the rows and the store's payload dicts on a helper thread, the store's normalisation of
+        # each encoder batch while the next one embeds; one upsert at the end as the reference's
+        # (same rows, same bytes)
+        def build_payloads():
+            rows = build_rows()
+            return rows, [LanceDBStore._payload(r) for r in rows]
+
+        fut = _row_builder().submit(build_payloads)
+        embeddings = vectors = None
         try:
-            parts = [(e, LanceDBStore._normalize_rows(e)) for e in embed_images_batches(paths)]
+            o = 0
+            for e in embed_images_batches(paths):
+                if embeddings is None:
+                    embeddings = np.empty((len(paths), e.shape[1]), np.float32)
+                    vectors = np.empty_like(embeddings)
+                embeddings[o:o + len(e)] = e
+                vectors[o:o + len(e)] = LanceDBStore._normalize_rows(e)
+                o += len(e)
         finally:
-            rows = fut.result()
-        embeddings = np.vstack([e for e, _ in parts])
+            rows, payloads = fut.result()
         for row, embedding in zip(rows, embeddings):
             row.embedding = embedding
-        _LANCEDB_STORE._upsert_image_normalized(rows, np.vstack([v for _, v in parts]))
+        _LANCEDB_STORE._upsert_image_payloads(payloads, vectors)
     else:
         rows = build_rows()
         embeddings = embed(paths)

@@ -236,20 +236,22 @@ class LanceDBStore:
         ``vectors``: ``_normalize_rows`` of the rows' embeddings when the caller already made it."""
         if vectors is None:
             vectors = LanceDBStore._normalize_rows(np.stack([np.asarray(r.embedding, dtype=np.float32) for r in rows]))
-        payloads = [
-            {
-                "chunk_id": row.chunk_id,
-                "user_id": row.user_id,
-                "document_id": row.document_id,
-                "modality": row.modality,
-                "embedding": vectors[i],
-                # index_image_nodes serialises the metadata on its helper thread while the images
-                # embed (index_build._meta_json); the same json.dumps otherwise
-                "meta": getattr(row, "_meta_json", None) or json.dumps(row.meta or {}),
-            }
-            for i, row in enumerate(rows)
-        ]
+        payloads = [LanceDBStore._payload(row) for row in rows]
+        for p, v in zip(payloads, vectors):
+            p["embedding"] = v
         return payloads, vectors
+
+    @staticmethod
+    def _payload(row: VectorRow) -> Dict[str, Any]:
+        """One row's ``_prepare_rows`` dict without its embedding (set by the caller)."""
+        return {
+            "chunk_id": row.chunk_id,
+            "user_id": row.user_id,
+            "document_id": row.document_id,
+            "modality": row.modality,
+            "embedding": None,
+            "meta": json.dumps(row.meta or {}),
+        }
 
     def _upsert(self, table: "_Table", rows: Iterable[VectorRow]) -> None:
         rows = list(rows)
@@ -260,11 +262,13 @@ class LanceDBStore:
         else:
             table.upsert(self._prepare_rows(rows))
 
-    def _upsert_image_normalized(self, rows: List[VectorRow], vectors: np.ndarray) -> None:
-        """``upsert_image_vectors(rows)`` when ``vectors`` already holds ``_normalize_rows`` of the
-        rows' embeddings (index_image_nodes computes it batch by batch while the images embed)."""
-        if rows:
-            payloads, vectors = self._prepare_rows_array(rows, vectors)
+    def _upsert_image_payloads(self, payloads: List[Dict[str, Any]], vectors: np.ndarray) -> None:
+        """``upsert_image_vectors(rows)`` from the rows' ``_payload`` dicts and ``vectors`` =
+        ``_normalize_rows`` of their embeddings (index_image_nodes makes both while the images
+        embed: the dicts on its helper thread, the normalisation per encoder batch)."""
+        if payloads:
+            for p, v in zip(payloads, vectors):
+                p["embedding"] = v
             self._image_table.upsert(payloads, vectors)
 
     def upsert_text_vectors(self, rows: Iterable[VectorRow]) -> None:

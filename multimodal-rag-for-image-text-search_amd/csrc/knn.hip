@@ -960,6 +960,7 @@ struct MergeParams {
   float* thresh;
   int32_t* fail_list;
   int32_t* fail_cnt;
+  int32_t* host_fail;  // coherent pinned host word set to 1 by a failing query (null: none)
   const uint32_t* theta;  // final shared threshold (rows at or below it were never listed)
   const float* part_tau;  // v3: [splits][Qp] bound on the rows each split list dropped (or null)
 };
@@ -1262,6 +1263,9 @@ __global__ __launch_bounds__(MERGE_THREADS) void knn_merge_kernel(MergeParams p)
       p.thresh[q] = (M >= p.k) ? f32_round_down(ex[p.k - 1] - EPS_F16) : -INFINITY;
       const int s = atomicAdd(p.fail_cnt, 1);
       p.fail_list[s] = q;
+      // the host reads this word after the stream completes and fetches the count only when
+      // it is set (no device-to-host copy behind a search that certifies every query)
+      if (p.host_fail) __hip_atomic_store(p.host_fail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
 #ifdef MRAG_K7_STAMPS
@@ -1624,6 +1628,7 @@ struct SearchCtx {
   DevBuf qin, q32, qn, q16, part_s, part_i, thresh, fail_list, counters, cand_cnt, cand, scratch;
   DevBuf out_s, out_s64, out_r, theta, part_tau;
   int32_t* host_counters = nullptr;  // pinned [2]: fail_cnt, overflow
+  int32_t* host_fail = nullptr;      // coherent pinned [4]: [0] = some query failed K8's certificate
   hipEvent_t done = nullptr;         // end of the search's device work (waited by spinning)
   hipEvent_t null_ev = nullptr;      // device inputs on the NULL stream: the search waits for it
   hipEvent_t ev0 = nullptr, ev1 = nullptr;  // scan timing (mrag_knn_profile)
@@ -1675,6 +1680,7 @@ void ctx_free_all(SearchCtx* c) {
     release(*b);
   mrag_knn::release(c->gws);
   if (c->host_counters) (void)hipHostFree(c->host_counters);
+  if (c->host_fail) (void)hipHostFree(c->host_fail);
   if (c->done) (void)hipEventDestroy(c->done);
   if (c->null_ev) (void)hipEventDestroy(c->null_ev);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -1694,6 +1700,7 @@ int ctx_get(mrag_knn_index* ix, SearchCtx** out) {
   }
   auto* c = new SearchCtx();
   hipError_t e = hipHostMalloc((void**)&c->host_counters, 16, hipHostMallocDefault);
+  if (e == hipSuccess) e = hipHostMalloc((void**)&c->host_fail, 16, hipHostMallocCoherent);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->done, hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->null_ev, hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreate(&c->ev0);
@@ -2109,6 +2116,8 @@ int mrag_knn_search(mrag_knn_index* ix, const float* queries, int64_t nq, int32_
     mp.fail_cnt = (int32_t*)c->counters.p;
     mp.theta = (const uint32_t*)c->theta.p;
     mp.part_tau = sp.part_tau;
+    mp.host_fail = c->host_fail;
+    __atomic_store_n(c->host_fail, 0, __ATOMIC_RELAXED);  // this context's previous search has completed
     // K8 key selection: the best M + 1 keys (the M candidates and the first one left out) by
     // the register top-64P fold when they fit, else the full bitonic sort (40.6 -> 36.5 us per
     // 1000-query search for the fold)
@@ -2119,13 +2128,20 @@ int mrag_knn_search(mrag_knn_index* ix, const float* queries, int64_t nq, int32_
     hipLaunchKernelGGL(merge, dim3((unsigned)nq), dim3(MERGE_THREADS), msh, s, mp);
     MRAG_CHECK_LAUNCH();
 
-    // The failure count, read back right after K8: the common search certifies every query and
-    // launches nothing more; otherwise K7c's grid is sized to the failing queries alone, with
+    // The failure count after K8: a failing query also raises the context's coherent host word,
+    // so the common search (every query certified) ends with the stream wait alone and the count
+    // is copied back only when the word is set (the 8-byte copy was a 4.4 us kernel per search);
+    // the common search launches nothing more; otherwise K7c's grid is sized to the failing queries alone, with
     // more splits than the main scan (one failing query over the main scan's 64 splits is one
     // 8-wave workgroup per split, latency-bound on its own LDS-DMA round trips: 0.3 ms over
     // 512k rows, notes/knn_scan_experiments.md)
-    MRAG_HIP(hipMemcpyAsync(c->host_counters, c->counters.p, 8, hipMemcpyDeviceToHost, s));
     if (int rc = wait_stream(c, s)) return rc;
+    if (__atomic_load_n(c->host_fail, __ATOMIC_ACQUIRE)) {
+      MRAG_HIP(hipMemcpyAsync(c->host_counters, c->counters.p, 8, hipMemcpyDeviceToHost, s));
+      if (int rc = wait_stream(c, s)) return rc;
+    } else {
+      c->host_counters[0] = 0;
+    }
     if (profile) {
       float ms = 0.f;
       MRAG_HIP(hipEventElapsedTime(&ms, c->ev0, c->ev1));
