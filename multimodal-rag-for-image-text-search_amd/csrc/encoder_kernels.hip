@@ -853,7 +853,9 @@ __global__ __launch_bounds__(WS_THREADS) void gemm_ws_kernel(GemmArgs g, int P, 
   f32x4 acc[2][4][NB];
   int m0_1 = 0, m0_2 = 0;  // first rows of tiles it - 1 (blocks written now) and it - 2 (rows stored now)
   // Epilogue through this wave's LDS output image (64 rows x 128 B; 8-byte unit u of row j at
-  // u ^ 2 (j & 7)): a block's four finished outputs (gemm_act of acc + bias: gemm_store4's
+  // u ^ 2 (j & 7): rows j and j + 8 of a ds_write_b64 lane group share a bank pair, 0.15 of the
+  // kernel's LDS cycles; the conflict-free u ^ (j & 15) needs the odd rows' unit pairs swapped
+  // back after the read and measured 2-4 % slower, profiles/r6s12_*): a block's four finished outputs (gemm_act of acc + bias: gemm_store4's
   // arithmetic) as one ds_write_b64, then whole 128-byte rows out by 16-byte global stores — one
   // store instruction = 8 rows x 128 B, 8 per tile, instead of 16 scattered 8-byte ones. During
   // tile it: k-steps 0-2 store tile it - 2's image (each row read a k-step before its store), the
