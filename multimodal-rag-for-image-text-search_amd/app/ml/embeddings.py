@@ -16,6 +16,7 @@ image batch is max(batch_size, 256) (results do not depend on it).
 from __future__ import annotations
 
 import os
+import time
 from pathlib import Path
 from typing import Any, Mapping, Optional, Sequence
 
@@ -104,16 +105,18 @@ def embed_images_batch(paths: Sequence[Path], batch_size: int = 8) -> np.ndarray
     return _normalize(np.vstack(list(_image_feature_batches(paths, batch_size))))
 
 
-def embed_images_batches(paths: Sequence[Path], batch_size: int = 8):
+def embed_images_batches(paths: Sequence[Path], batch_size: int = 8, idle=None):
     """``embed_images_batch`` one encoder batch at a time: yields the normalised rows of each
-    batch in order, while the next batches' files are read and decoded on the pipeline's threads
-    (index_image_nodes prepares the store's rows of batch i while batch i + 1 encodes). The rows
-    equal embed_images_batch's: ``_normalize`` reduces each row on its own."""
-    for raw in _image_feature_batches(paths, batch_size):
+    batch in order, while the next batches' files are read and decoded on the pipeline's threads.
+    The rows equal embed_images_batch's: ``_normalize`` reduces each row on its own. ``idle``: a
+    callable run while this thread would wait for the next decoded batch, repeatedly as long as it
+    returns True (index_image_nodes builds the store's rows there: on this thread, so its Python
+    does not contend for the interpreter lock with the pipeline's own threads)."""
+    for raw in _image_feature_batches(paths, batch_size, idle):
         yield _normalize(raw)
 
 
-def _image_feature_batches(paths: Sequence[Path], batch_size: int):
+def _image_feature_batches(paths: Sequence[Path], batch_size: int, idle=None):
     """The vision tower's unnormalised features, one array per encoder batch."""
     if not paths:
         return
@@ -164,7 +167,11 @@ def _image_feature_batches(paths: Sequence[Path], batch_size: int):
                 dec(i)
                 dec(i + 1)
                 prep(i + 2)
-                n_i, imgs = decs.pop(i).result()
+                fut_i = decs.pop(i)
+                if idle is not None:
+                    while not fut_i.done() and idle():
+                        time.sleep(0)  # lets the pipeline's threads take the interpreter lock
+                n_i, imgs = fut_i.result()
                 preps.pop(i, None)
                 for c0 in range(0, n_i, step):
                     inputs = processor.from_device(imgs, c0, step)

@@ -23,6 +23,7 @@ import numpy as np
 from app.ml.embeddings import embed_images_batch, embed_images_batches, embed_query_for_images, embed_text_batch
 from app.ml.splitter import Document, SentenceSplitter
 from app.settings import settings
+from app.storage.corpus_files import CorpusFiles
 from app.storage.lancedb_store import LanceDBStore, VectorRow
 
 _SPLITTER = SentenceSplitter(chunk_size=512, chunk_overlap=64)
@@ -143,16 +144,6 @@ def _paths_exist(strs: List[str]) -> List[bool]:
 
 
 _FS_ENCODING = sys.getfilesystemencoding()
-_ROW_BUILDER = None  # one helper thread, kept: starting a thread per call cost ~1-5 ms
-
-
-def _row_builder():
-    global _ROW_BUILDER
-    if _ROW_BUILDER is None:
-        from concurrent.futures import ThreadPoolExecutor
-
-        _ROW_BUILDER = ThreadPoolExecutor(max_workers=1, thread_name_prefix="mrag-rows")
-    return _ROW_BUILDER
 
 
 def index_image_nodes(user_id: str, nodes: Sequence[Dict[str, object]]) -> List[Dict[str, object]]:
@@ -160,8 +151,10 @@ def index_image_nodes(user_id: str, nodes: Sequence[Dict[str, object]]) -> List[
 
     The reference's per-node loop (:110-126) as three steps with the same result: the metadata
     copies and file paths, the existence filter as one library call (_paths_exist), then the
-    VectorRows built on a helper thread while this one embeds the files (this package's
-    embed_images_batch takes the paths as strings; a substituted one gets Path objects)."""
+    embed. With this package's embed and store (>= 256 files) the rows' metadata, the store's
+    payload dicts and their Parquet are made while the embed pipeline waits for its next decoded
+    batch, and each embedded batch is normalised for the store there too (embed_images_batches);
+    otherwise the reference's order (a substituted embed_images_batch gets Path objects)."""
     metas = [dict(node.get("metadata", {})) for node in nodes]
     strs = [str(m.get("file_path", "")) for m in metas]
     sel = [i for i, e in enumerate(_paths_exist(strs)) if e]
@@ -171,9 +164,9 @@ def index_image_nodes(user_id: str, nodes: Sequence[Dict[str, object]]) -> List[
     native = embed is _EMBED_IMAGES_NATIVE
     paths = [strs[i] for i in sel] if native else [Path(strs[i]) for i in sel]
 
-    def build_rows() -> List[VectorRow]:
+    def build_rows(idx: List[int]) -> List[VectorRow]:
         out = []
-        for i in sel:
+        for i in idx:
             metadata = metas[i]
             chunk_id = str(nodes[i].get("id"))
             metadata.update({"doc_id": metadata.get("doc_id", chunk_id), "user_id": user_id, "modality": "image",
@@ -184,35 +177,56 @@ def index_image_nodes(user_id: str, nodes: Sequence[Dict[str, object]]) -> List[
 
     array_rows = _array_rows()
     if native and array_rows and len(sel) >= 256:
-        # the rows and the store's payload dicts on a helper thread, the store's normalisation of
-        # each encoder batch while the next one embeds; one upsert at the end as the reference's
-        # (same rows, same bytes)
-        def build_payloads():
-            rows = build_rows()
-            return rows, [LanceDBStore._payload(r) for r in rows]
-
-        fut = _row_builder().submit(build_payloads)
+        # while this thread would wait for the pipeline's next decoded batch: the store's
+        # normalisation of the batches already embedded, then the rows and the store's payload
+        # dicts in chunks; one upsert at the end as the reference's (same rows, same bytes)
+        out, payloads, pending, staged = [], [], [], []
         embeddings = vectors = None
+
+        def chunks():
+            for c0 in range(0, len(sel), 128):
+                for i in sel[c0:c0 + 128]:
+                    metadata = metas[i]
+                    chunk_id = str(nodes[i].get("id"))
+                    metadata.update({"doc_id": metadata.get("doc_id", chunk_id), "user_id": user_id,
+                                     "modality": "image", "source": metadata.get("source")})
+                    payloads.append(LanceDBStore._payload(chunk_id, user_id, metadata["doc_id"], "image", metadata))
+                    out.append({"chunk_id": chunk_id, "metadata": metadata})
+                yield
+            staged.append(_LANCEDB_STORE._stage_image_payloads(payloads))  # the Parquet, ahead of the upsert
+            yield
+
+        work = chunks()
+
+        def idle() -> bool:
+            if pending:
+                o, m = pending.pop()
+                vectors[o:o + m] = LanceDBStore._normalize_rows(embeddings[o:o + m])
+                return True
+            return next(work, False) is None
+
         try:
             o = 0
-            for e in embed_images_batches(paths):
+            for e in embed_images_batches(paths, idle=idle):
                 if embeddings is None:
                     embeddings = np.empty((len(paths), e.shape[1]), np.float32)
                     vectors = np.empty_like(embeddings)
                 embeddings[o:o + len(e)] = e
-                vectors[o:o + len(e)] = LanceDBStore._normalize_rows(e)
+                pending.append((o, len(e)))
                 o += len(e)
-        finally:
-            rows, payloads = fut.result()
-        for row, embedding in zip(rows, embeddings):
-            row.embedding = embedding
-        _LANCEDB_STORE._upsert_image_payloads(payloads, vectors)
-    else:
-        rows = build_rows()
-        embeddings = embed(paths)
-        for row, embedding in zip(rows, embeddings):
-            row.embedding = _row_embedding(embedding, array_rows)
-        _LANCEDB_STORE.upsert_image_vectors(rows)
+            while idle():  # what the waits left
+                pass
+        except BaseException:
+            CorpusFiles.discard_staged(staged[0] if staged else None)
+            raise
+        _LANCEDB_STORE._upsert_image_payloads(payloads, vectors, staged[0])
+        _bump_version(user_id)
+        return out
+    rows = build_rows(sel)
+    embeddings = embed(paths)
+    for row, embedding in zip(rows, embeddings):
+        row.embedding = _row_embedding(embedding, array_rows)
+    _LANCEDB_STORE.upsert_image_vectors(rows)
     _bump_version(user_id)
     return [{"chunk_id": row.chunk_id, "metadata": row.meta} for row in rows]
 

@@ -39,7 +39,7 @@ import numpy as np
 COLUMNS = ("chunk_id", "user_id", "document_id", "modality", "meta")
 
 
-def _fsync_write(path: str, data: bytes) -> None:
+def _fsync_write(path: str, data) -> None:
     tmp = path + ".tmp"
     with open(tmp, "wb") as f:
         f.write(data)
@@ -99,15 +99,47 @@ class CorpusFiles:
     def num_rows(self) -> int:
         return sum(s["rows"] for s in self.manifest["segments"])
 
-    def append(self, vectors: np.ndarray, rows: Sequence[Dict[str, Any]], dead: Sequence[int] = ()) -> None:
+    def stage_rows(self, rows: Sequence[Dict[str, Any]]) -> str:
+        """The payload Parquet of an upcoming ``append``, written and fsynced ahead of it under a
+        unique staging name in the table directory (index_image_nodes writes it while its images
+        embed); ``append(..., staged=path)`` renames it into place. Not listed by any manifest
+        until then; ``discard_staged`` removes it."""
+        import tempfile
+
+        import pyarrow as pa
+        import pyarrow.parquet as pq
+
+        os.makedirs(self.dir, exist_ok=True)
+        fd, path = tempfile.mkstemp(prefix=".stage_", suffix=".parquet", dir=self.dir)
+        os.close(fd)
+        try:
+            pq.write_table(pa.table({c: [str(r[c]) for r in rows] for c in COLUMNS}), path)
+            with open(path, "rb") as f:
+                os.fsync(f.fileno())
+        except BaseException:
+            self.discard_staged(path)
+            raise
+        return path
+
+    @staticmethod
+    def discard_staged(path: Optional[str]) -> None:
+        if path:
+            with contextlib.suppress(FileNotFoundError):
+                os.unlink(path)
+
+    def append(self, vectors: np.ndarray, rows: Sequence[Dict[str, Any]], dead: Sequence[int] = (),
+               staged: Optional[str] = None) -> None:
         """Durably append one upsert: its tombstones (row ids it replaces) and its rows. Call
-        it inside ``write_lock()`` when other processes may write the same table."""
+        it inside ``write_lock()`` when other processes may write the same table. ``staged``:
+        the rows' Parquet from ``stage_rows`` (moved into place instead of written here)."""
         import pyarrow as pa
         import pyarrow.parquet as pq
 
         v = np.ascontiguousarray(vectors, dtype="<f4")
         if v.ndim != 2 or v.shape[0] != len(rows):
             raise ValueError("vectors must be [n, dim] with one payload row each")
+        if staged is not None and pq.read_metadata(staged).num_rows != v.shape[0]:
+            raise ValueError("staged payloads do not match the vectors")
         m = json.loads(json.dumps(self.manifest))  # committed to self.manifest only on success
         if m["dim"] is None:
             m["dim"] = int(v.shape[1])
@@ -127,12 +159,15 @@ class CorpusFiles:
             m["tombstones"] += len(dead)
         if v.shape[0]:
             name = f"seg_{len(m['segments']):06d}"
-            _fsync_write(os.path.join(self.dir, name + ".f32"), v.tobytes())
-            table = pa.table({c: [str(r[c]) for r in rows] for c in COLUMNS})
-            tmp = os.path.join(self.dir, name + ".parquet.tmp")
-            pq.write_table(table, tmp)
-            with open(tmp, "rb") as f:
-                os.fsync(f.fileno())
+            _fsync_write(os.path.join(self.dir, name + ".f32"), v.data)  # the array's bytes, no copy
+            if staged is not None:
+                tmp = staged
+            else:
+                table = pa.table({c: [str(r[c]) for r in rows] for c in COLUMNS})
+                tmp = os.path.join(self.dir, name + ".parquet.tmp")
+                pq.write_table(table, tmp)
+                with open(tmp, "rb") as f:
+                    os.fsync(f.fileno())
             os.replace(tmp, os.path.join(self.dir, name + ".parquet"))
             m["segments"].append({"name": name, "rows": int(v.shape[0])})
         _fsync_write(self.manifest_path, json.dumps(m).encode())

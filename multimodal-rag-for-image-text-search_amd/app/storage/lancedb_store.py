@@ -30,6 +30,8 @@ from typing import Any, Dict, Iterable, List, Optional, Sequence
 
 import numpy as np
 
+from app.storage.corpus_files import CorpusFiles
+
 
 @dataclass
 class VectorRow:
@@ -122,9 +124,17 @@ class _Table:
 
     _load = _sync  # name used by app.retrieval
 
-    def upsert(self, payloads: List[Dict[str, Any]], vectors: Optional[np.ndarray] = None) -> None:
+    def upsert(self, payloads: List[Dict[str, Any]], vectors: Optional[np.ndarray] = None,
+               staged: Optional[str] = None) -> None:
         """Per-row delete of the payloads' chunk ids, then one append. ``vectors`` (f32 [n, dim]):
-        the payloads' embeddings already stacked (the array path of LanceDBStore._upsert)."""
+        the payloads' embeddings already stacked (the array path of LanceDBStore._upsert);
+        ``staged``: their Parquet from CorpusFiles.stage_rows (removed if the append fails)."""
+        try:
+            self._upsert(payloads, vectors, staged)
+        finally:
+            CorpusFiles.discard_staged(staged)  # renamed into place by a successful append
+
+    def _upsert(self, payloads, vectors, staged) -> None:
         if not payloads:
             return
         with self.lock:
@@ -142,7 +152,7 @@ class _Table:
                 for p in payloads:
                     dead.extend(self.by_chunk.get(p["chunk_id"], []))
                 if self.files is not None:  # durable first: a failed write leaves the table as it was
-                    self.files.append(emb, payloads, dead)
+                    self.files.append(emb, payloads, dead, staged)
                     self._seen_segments += 1
                     self._seen_tombstones += len(dead)
                 self._kill_rows(dead)
@@ -236,21 +246,22 @@ class LanceDBStore:
         ``vectors``: ``_normalize_rows`` of the rows' embeddings when the caller already made it."""
         if vectors is None:
             vectors = LanceDBStore._normalize_rows(np.stack([np.asarray(r.embedding, dtype=np.float32) for r in rows]))
-        payloads = [LanceDBStore._payload(row) for row in rows]
+        payloads = [LanceDBStore._payload(row.chunk_id, row.user_id, row.document_id, row.modality, row.meta)
+                    for row in rows]
         for p, v in zip(payloads, vectors):
             p["embedding"] = v
         return payloads, vectors
 
     @staticmethod
-    def _payload(row: VectorRow) -> Dict[str, Any]:
+    def _payload(chunk_id: str, user_id: str, document_id: str, modality: str, meta) -> Dict[str, Any]:
         """One row's ``_prepare_rows`` dict without its embedding (set by the caller)."""
         return {
-            "chunk_id": row.chunk_id,
-            "user_id": row.user_id,
-            "document_id": row.document_id,
-            "modality": row.modality,
+            "chunk_id": chunk_id,
+            "user_id": user_id,
+            "document_id": document_id,
+            "modality": modality,
             "embedding": None,
-            "meta": json.dumps(row.meta or {}),
+            "meta": json.dumps(meta or {}),
         }
 
     def _upsert(self, table: "_Table", rows: Iterable[VectorRow]) -> None:
@@ -262,14 +273,23 @@ class LanceDBStore:
         else:
             table.upsert(self._prepare_rows(rows))
 
-    def _upsert_image_payloads(self, payloads: List[Dict[str, Any]], vectors: np.ndarray) -> None:
+    def _stage_image_payloads(self, payloads: List[Dict[str, Any]]) -> Optional[str]:
+        """The image table's Parquet of ``payloads`` written ahead of their upsert (None for an
+        in-memory table)."""
+        files = self._image_table.files
+        return files.stage_rows(payloads) if files is not None and payloads else None
+
+    def _upsert_image_payloads(self, payloads: List[Dict[str, Any]], vectors: np.ndarray,
+                               staged: Optional[str] = None) -> None:
         """``upsert_image_vectors(rows)`` from the rows' ``_payload`` dicts and ``vectors`` =
-        ``_normalize_rows`` of their embeddings (index_image_nodes makes both while the images
-        embed: the dicts on its helper thread, the normalisation per encoder batch)."""
+        ``_normalize_rows`` of their embeddings (index_image_nodes makes both, and the staged
+        Parquet, while the images embed)."""
         if payloads:
             for p, v in zip(payloads, vectors):
                 p["embedding"] = v
-            self._image_table.upsert(payloads, vectors)
+            self._image_table.upsert(payloads, vectors, staged)
+        else:
+            CorpusFiles.discard_staged(staged)
 
     def upsert_text_vectors(self, rows: Iterable[VectorRow]) -> None:
         self._upsert(self._text_table, rows)

@@ -54,3 +54,48 @@ def test_manifest_is_the_commit_point(tmp_path):
     h = CorpusFiles(d)
     assert h.num_rows == 3 and h.tombstones().tolist() == [1]
     assert np.asarray(list(h.segments())[1].vectors).tolist() == [[2.0] * 4]
+
+
+def test_staged_payloads_commit_like_written_ones(tmp_path):
+    """stage_rows (index_image_nodes writes the Parquet while its images embed) then
+    append(..., staged=...) gives the same files as a plain append; a staged file that does not
+    match its vectors is refused and, through _Table.upsert, removed; nothing stays behind."""
+    from app.storage.corpus_files import CorpusFiles
+
+    v = np.arange(12, dtype=np.float32).reshape(3, 4)
+    a, b = CorpusFiles(str(tmp_path / "a")), CorpusFiles(str(tmp_path / "b"))
+    a.append(v, _rows(["x", "y", "z"]))
+    path = b.stage_rows(_rows(["x", "y", "z"]))
+    assert os.path.exists(path) and CorpusFiles(str(tmp_path / "b")).num_rows == 0  # not committed yet
+    b.append(v, _rows(["x", "y", "z"]), staged=path)
+    assert not os.path.exists(path)
+    for name in ("seg_000000.parquet", "seg_000000.f32"):
+        ra = open(os.path.join(a.dir, name), "rb").read()
+        rb = open(os.path.join(b.dir, name), "rb").read()
+        assert ra == rb, name
+    bad = b.stage_rows(_rows(["p", "q"]))
+    with pytest.raises(ValueError):
+        b.append(v, _rows(["x", "y", "z"]), staged=bad)
+    CorpusFiles.discard_staged(bad)
+    assert sorted(f for f in os.listdir(b.dir) if f.startswith(".stage_")) == []
+    assert CorpusFiles(b.dir).num_rows == 3
+
+
+def test_table_upsert_removes_a_refused_staged_file(tmp_path):
+    from app.storage.corpus_files import CorpusFiles
+    from app.storage.lancedb_store import _Table
+
+    t = _Table("image_collection", 0, str(tmp_path / "img"))
+    staged = t.files.stage_rows(_rows(["p"]))
+
+    class Boom(Exception):
+        pass
+
+    def boom(*a, **k):
+        raise Boom()
+
+    t._sync = boom  # fails under the writer lock, before the append
+    with pytest.raises(Boom):
+        t.upsert(_rows(["p"]), np.ones((1, 4), np.float32), staged)
+    assert not os.path.exists(staged)
+    assert CorpusFiles(t.files.dir).num_rows == 0
