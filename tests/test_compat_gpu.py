@@ -409,3 +409,34 @@ def test_index_image_nodes_batched_rows_equal_reference_form(cuda, tmp_path, mon
     metas = [{"file_path": str(tmp_path / f"f{i}.{'png' if i % 4 == 0 else 'jpg'}"), "page": i, "doc_id": f"n{i}",
               "user_id": "u1", "modality": "image", "source": None} for i in present]
     assert segs[0].rows["meta"] == [json.dumps(m) for m in metas]
+
+
+def test_index_image_nodes_batched_failure_commits_nothing(cuda, tmp_path, monkeypatch):
+    """A file Pillow cannot read in the batched form (300 files): index_image_nodes raises what
+    embed_images_batch raises for the same paths (the reference's embed raises before its upsert),
+    the table gains no rows, no staged Parquet stays behind and the version is not bumped."""
+    import os
+
+    from app.ml import embeddings, index_build
+    from app.storage.lancedb_store import LanceDBStore
+
+    store = LanceDBStore(str(tmp_path / "db4"))
+    monkeypatch.setattr(index_build, "_LANCEDB_STORE", store)
+    monkeypatch.setattr(index_build, "_VERSION_FILE", tmp_path / "versions.json")
+    rng = np.random.default_rng(5)
+    paths = []
+    for i in range(300):
+        p = tmp_path / f"g{i}.png"
+        Image.fromarray(rng.integers(0, 256, (48, 40, 3), dtype=np.uint8)).save(p)
+        paths.append(p)
+    paths[260].write_bytes(b"not an image at all")
+    with pytest.raises(Exception) as ref_err:
+        embeddings.embed_images_batch([str(p) for p in paths])
+    nodes = [{"id": f"m{i}", "metadata": {"file_path": str(p)}} for i, p in enumerate(paths)]
+    with pytest.raises(type(ref_err.value)):
+        index_build.index_image_nodes("u2", nodes)
+    files = store._image_table.files
+    assert files is None or files.num_rows == 0
+    d = os.path.join(str(tmp_path / "db4"), "mrag_tables", "image_collection")
+    assert not os.path.isdir(d) or not [f for f in os.listdir(d) if f.startswith(".stage_")]
+    assert index_build.get_index_version("u2") == 0
