@@ -99,10 +99,19 @@ def _get_embeddings(query: str) -> Tuple[np.ndarray, np.ndarray]:
     encodes are independent chains of small kernels, so the CLIP-text one runs in a worker thread
     on its own HIP stream while this thread runs MiniLM (the pair takes ~the longer of the two
     instead of their sum; the vectors are the same, and an exception from either propagates)."""
+    text_vec, finish = _text_embedding_first(query)
+    return text_vec, finish()
+
+
+def _text_embedding_first(query: str):
+    """``_get_embeddings`` in two halves: the MiniLM vector now, and ``finish()`` -> the CLIP-text
+    vector, which also fills the query-embedding cache exactly as ``_get_embeddings`` does.
+    retrieve_text runs its search and chunk lookup between the two (they need only the MiniLM
+    vector), while the CLIP-text encode is still running on its own stream."""
     global _QUERY_POOL
     cached = get_query_embeddings(query)
     if cached:
-        return cached
+        return cached[0], (lambda: cached[1])
     import torch
 
     fut = None
@@ -118,11 +127,18 @@ def _get_embeddings(query: str) -> Tuple[np.ndarray, np.ndarray]:
         if fut is not None:
             fut.exception()  # let the image branch finish; the text error is the one raised
         raise
-    image_vec = fut.result() if fut is not None else embed_query_for_images(query)
-    set_query_embeddings(query, text_vec[0] if text_vec.size else np.zeros(384, dtype=np.float32), image_vec)
-    if text_vec.size == 0:
-        text_vec = np.zeros((1, 384), dtype=np.float32)
-    return text_vec[0], image_vec
+
+    early = embed_query_for_images(query) if fut is None else None  # no worker: the reference's order
+
+    def finish() -> np.ndarray:
+        image_vec = fut.result() if fut is not None else early
+        set_query_embeddings(query, text_vec[0] if text_vec.size else np.zeros(384, dtype=np.float32), image_vec)
+        return image_vec
+
+    return (text_vec[0] if text_vec.size else np.zeros(384, dtype=np.float32)), finish
+
+
+_GET_EMBEDDINGS = _get_embeddings  # this module's own; a rebound global is honoured by retrieve_text
 
 
 def _chunks_for(hits: List[Dict[str, Any]]) -> List[Optional[Chunk]]:
@@ -143,12 +159,29 @@ def retrieve_text(user_id: str, query: str, top_k: Optional[int] = None) -> List
     cached = get_retrieval_results(user_id, f"text::{query}", version)
     if cached is not None:
         return cached
-    text_vec, _ = _get_embeddings(query)
+    # the search and the hits' chunks run while the CLIP-text query encode (needed only by
+    # retrieve_images) finishes on its own stream; both vectors are in the cache before this
+    # returns or raises, as after the reference's _get_embeddings (an error of the CLIP-text
+    # encode is the one raised, as there: it would have stopped the reference before the search)
+    if _get_embeddings is _GET_EMBEDDINGS:
+        text_vec, finish = _text_embedding_first(query)
+    else:  # a substituted _get_embeddings (a test seam) is called as the reference calls it
+        text_vec, _ = _get_embeddings(query)
+        finish = lambda: None  # noqa: E731
+    try:
+        if text_vec.size == 0:
+            hits, chunks = [], []
+        else:
+            hits = _LANCEDB_STORE.search_text(user_id, text_vec.tolist(), top_k)
+            chunks = _chunks_for(hits)
+    except BaseException:
+        finish()
+        raise
+    finish()
     if text_vec.size == 0:
         return []
     results: List[Dict[str, Any]] = []
-    hits = _LANCEDB_STORE.search_text(user_id, text_vec.tolist(), top_k)
-    for entry, chunk in zip(hits, _chunks_for(hits)):
+    for entry, chunk in zip(hits, chunks):
         if not chunk or not chunk.text:
             continue
         results.append({"chunk_id": chunk.id, "modality": "text", "score": float(entry["score"]),
