@@ -5,8 +5,9 @@ the contiguous global rows [row_offset_r, row_offset_r + n_r) in its own
 ``FlatIndex``. A search is:
 
   1. local exact top-k on every rank (K7/K8/K10; global row ids via row_offset);
-  2. ONE all-gather of the per-shard (f64 score, int64 row) lists, [world, nq, k]
-     (1000 x 10 x 16 B = 160 KB per rank: latency-bound, far below the scan time);
+  2. ONE all-gather of the per-shard (f64 score, int64 row) lists packed as 16-byte records,
+     [world, nq, k, 2] (1000 x 10 x 16 B = 160 KB per rank: latency-bound, far below the scan
+     time; one collective per step, not one per list);
   3. the K11 merge under (score desc, row asc) — identical to a single-index search
      because every shard's list is its exact top-k.
 
@@ -71,8 +72,18 @@ class ShardedFlatIndex:
             cur = torch.cuda.current_stream(s64.device)
             for t in (s64, r):
                 t.record_stream(cur)
-        ms, mr, _ = self._merge(self._gather(s64), self._gather(r), k)
+        ms, mr, _ = self._merge(*self._gather_hits(s64, r), k)
         return ms, mr
+
+    def _gather_hits(self, s64, r):
+        """Every rank's (f64 scores, int64 rows) lists as [world, nq, k] each, in ONE collective:
+        a hit's score (its 8 bytes as int64) and row travel as one 16-byte record, [nq, k, 2],
+        split back bit for bit."""
+        import torch
+
+        packed = torch.stack((s64.contiguous().view(torch.int64), r.to(torch.int64)), dim=-1)
+        g = self._gather(packed)
+        return g[..., 0].contiguous().view(torch.float64), g[..., 1].contiguous()
 
 
 __all__ = ["ShardedFlatIndex"]

@@ -71,6 +71,11 @@ def test_rccl_gather_then_k11_equals_single_index(rccl_world1, dim, k, nq):
         assert g64.is_cuda and gr.is_cuda
         torch.cuda.synchronize()
         assert torch.equal(g64[0], s64) and torch.equal(gr[0], r)  # world 1: the gather is a copy
+        # combine's form: scores and rows packed as 16-byte records, one all-gather, split back
+        p64, pr = sh._gather_hits(s64, r)
+        torch.cuda.synchronize()
+        assert p64.dtype == torch.float64 and pr.dtype == torch.int64
+        assert torch.equal(p64, g64) and torch.equal(pr, gr)
         gathered_s.append(g64)
         gathered_r.append(gr)
 
