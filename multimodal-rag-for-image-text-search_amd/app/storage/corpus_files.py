@@ -86,10 +86,28 @@ class CorpusFiles:
         try:
             fcntl.flock(fd, fcntl.LOCK_EX)
             self.refresh()
+            self._drop_stale_stages()
             yield self
         finally:
             fcntl.flock(fd, fcntl.LOCK_UN)
             os.close(fd)
+
+    STALE_STAGE_S = 24 * 3600  # a staged Parquet this old belonged to a writer that died
+
+    def _drop_stale_stages(self) -> None:
+        """Remove ``stage_rows`` files a crashed writer left (never listed by a manifest); a live
+        writer's staged file is younger than any index call (it is written while that call's
+        images embed and renamed at its commit)."""
+        import time
+
+        now = time.time()
+        with contextlib.suppress(OSError):
+            for name in os.listdir(self.dir):
+                if name.startswith(".stage_") and name.endswith(".parquet"):
+                    path = os.path.join(self.dir, name)
+                    with contextlib.suppress(OSError):
+                        if now - os.stat(path).st_mtime > self.STALE_STAGE_S:
+                            os.unlink(path)
 
     @property
     def dim(self) -> Optional[int]:

@@ -99,3 +99,22 @@ def test_table_upsert_removes_a_refused_staged_file(tmp_path):
         t.upsert(_rows(["p"]), np.ones((1, 4), np.float32), staged)
     assert not os.path.exists(staged)
     assert CorpusFiles(t.files.dir).num_rows == 0
+
+
+def test_stale_staged_files_are_dropped_by_the_next_writer(tmp_path):
+    """A staged Parquet left by a writer that died (older than STALE_STAGE_S) is removed under
+    the next writer lock; a fresh one (a live writer's) stays."""
+    import time
+
+    from app.storage.corpus_files import CorpusFiles
+
+    f = CorpusFiles(str(tmp_path / "t"))
+    old = f.stage_rows(_rows(["a"]))
+    fresh = f.stage_rows(_rows(["b"]))
+    past = time.time() - CorpusFiles.STALE_STAGE_S - 60
+    os.utime(old, (past, past))
+    with f.write_lock():
+        pass
+    assert not os.path.exists(old) and os.path.exists(fresh)
+    f.append(np.ones((1, 4), np.float32), _rows(["b"]), staged=fresh)
+    assert CorpusFiles(f.dir).num_rows == 1
