@@ -62,6 +62,7 @@ class CorpusFiles:
         self.manifest_path = os.path.join(directory, "manifest.json")
         self.manifest: Dict[str, Any] = {"dim": None, "segments": [], "tombstones": 0}
         self._stamp = None
+        self._stages_checked = False
         self.refresh()
 
     def refresh(self) -> bool:
@@ -86,7 +87,9 @@ class CorpusFiles:
         try:
             fcntl.flock(fd, fcntl.LOCK_EX)
             self.refresh()
-            self._drop_stale_stages()
+            if not self._stages_checked:  # once per process and table: a listdir of the segments
+                self._stages_checked = True
+                self._drop_stale_stages()
             yield self
         finally:
             fcntl.flock(fd, fcntl.LOCK_UN)
