@@ -440,3 +440,25 @@ def test_index_image_nodes_batched_failure_commits_nothing(cuda, tmp_path, monke
     d = os.path.join(str(tmp_path / "db4"), "mrag_tables", "image_collection")
     assert not os.path.isdir(d) or not [f for f in os.listdir(d) if f.startswith(".stage_")]
     assert index_build.get_index_version("u2") == 0
+
+
+def test_embed_images_batches_equal_embed_images_batch(cuda, tmp_path):
+    """embed_images_batches (index_image_nodes' form: one encoder batch at a time, an idle
+    callback run while the pipeline waits) yields, stacked, the bytes of embed_images_batch."""
+    from app.ml import embeddings
+
+    rng = np.random.default_rng(6)
+    paths = []
+    for i in range(520):
+        p = tmp_path / f"h{i}.{'png' if i % 3 == 0 else 'jpg'}"
+        Image.fromarray(rng.integers(0, 256, (30 + i % 17, 36 + i % 13, 3), dtype=np.uint8)).save(p)
+        paths.append(str(p))
+    calls = []
+
+    def idle():
+        calls.append(1)
+        return len(calls) < 1000
+
+    parts = list(embeddings.embed_images_batches(paths, idle=idle))
+    assert [len(p) for p in parts] == [256, 256, 8]
+    assert np.array_equal(np.vstack(parts), embeddings.embed_images_batch(paths))
