@@ -37,3 +37,24 @@ def test_pair_tokenisation_matches_hf_tokenizer(tmp_path):
     np.testing.assert_array_equal(ids, ref["input_ids"])
     np.testing.assert_array_equal(types, ref["token_type_ids"])
     np.testing.assert_array_equal(mask, ref["attention_mask"])
+
+
+def test_single_text_tokenisation_matches_hf_tokenizer(tmp_path):
+    """MiniLM's tokeniser with a vocabulary (one text, and a batch through encode_batch) gives the
+    HF fast tokenizer's ids and mask with truncation=True at max_length, as sentence-transformers
+    calls it (reference app/ml/embeddings.py:62-67)."""
+    from transformers import BertTokenizerFast
+
+    from app.encoders.tokenize import WordPieceTokenizer
+
+    words = ["alpha", "beta", "gamma", "delta", "eps", "zeta", "eta", "theta", "##s", "x", "y"]
+    (tmp_path / "vocab.txt").write_text("\n".join(["[PAD]", "[UNK]", "[CLS]", "[SEP]", "[MASK]"] + words) + "\n")
+    ours = WordPieceTokenizer(str(tmp_path), max_len=8)
+    hf = BertTokenizerFast(str(tmp_path / "vocab.txt"), do_lower_case=True)
+    texts = ["alpha beta", "gamma delta eps zeta eta theta x y alpha beta gamma", "Alphas, beta!", "unknownword x"]
+    ids, mask = ours(texts)
+    ref = hf(texts, padding=True, truncation=True, max_length=8, return_tensors="np")
+    np.testing.assert_array_equal(ids, ref["input_ids"])
+    np.testing.assert_array_equal(mask, ref["attention_mask"])
+    for t in texts:
+        assert ours.encode_one(t) == hf(t, truncation=True, max_length=8)["input_ids"]
