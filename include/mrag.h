@@ -278,6 +278,16 @@ int mrag_files_free(mrag_files* files);
  * Path.exists ignores), -1 (any other error: the caller asks Path.exists, which raises it). */
 int mrag_paths_exist(const char* const* paths, int32_t n, int32_t threads, int32_t* out);
 
+/* mrag_hash_tokenize: the offline stand-in tokeniser of app/encoders/tokenize.py (no local
+ * vocabulary: the reference's sentence-transformers / CLIPProcessor tokenisers, app/ml/
+ * embeddings.py:62-67 / :100-103, cannot load their hub vocabularies offline) for ASCII texts, on
+ * `threads` host threads: the tokens of `\w+|[^\w\s]` over the lowercased text, each id = lo +
+ * crc32(token) % (hi - lo), at most max_tokens per text, into ids[i * max_tokens ...];
+ * counts[i] = the number written, or -1 when text i (texts[i], lens[i] bytes) holds a non-ASCII
+ * byte (the caller tokenises it in Python: NFC and Unicode classes). */
+int mrag_hash_tokenize(const char* const* texts, const int64_t* lens, int32_t n, int32_t lo, int32_t hi,
+                       int32_t max_tokens, int32_t threads, int32_t* ids, int32_t* counts);
+
 /* K3 building block: C[M][N] (op)= A[M][K] . W[N][K]^T + bias (device pointers;
  * A, W fp16 row-major; epilogue 0 f16 out, 1 f16 quick_gelu, 2 f16 gelu_erf,
  * 3 f32 C += , 4 f32 out). N % 128 == 0, K % 64 == 0; bias and C 16-byte aligned. */

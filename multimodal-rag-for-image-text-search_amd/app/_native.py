@@ -57,6 +57,7 @@ SIGNATURES = {
     "mrag_files_decode": (_c_int, [_vp, _vp, _vp, _c_int, _vp]),
     "mrag_files_free": (_c_int, [_vp]),
     "mrag_paths_exist": (_c_int, [_vp, _c_int, _c_int, _vp]),
+    "mrag_hash_tokenize": (_c_int, [_vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp]),
 }
 
 _lib: Optional[ctypes.CDLL] = None

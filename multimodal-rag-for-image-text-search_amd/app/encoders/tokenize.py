@@ -58,6 +58,60 @@ class _HashIds:
         return out
 
 
+_NATIVE_MIN = 16  # texts per call from which the library's ASCII path is used
+
+
+def _hash_bodies(texts: Sequence[str], ids_of, cap: int) -> Tuple[np.ndarray, np.ndarray]:
+    """The hashed token ids of every text, at most ``cap`` per text, as a [n, cap] int32 matrix
+    and the per-text counts: ASCII texts through the library (mrag_hash_tokenize: the same tokens
+    and crc32 as _basic_tokens + _hash_id, on its own threads) when there are enough of them,
+    every other text (and every text without the library) through the Python path ``ids_of``."""
+    n = len(texts)
+    body = np.zeros((n, cap), dtype=np.int32)
+    counts = np.full(n, -1, dtype=np.int32)
+    asc = [i for i, t in enumerate(texts) if t.isascii()]
+    if len(asc) >= _NATIVE_MIN:
+        try:
+            import ctypes
+
+            from app import _native
+            from app.encoders.preprocess import decode_workers
+
+            bufs = [texts[i].encode("ascii") for i in asc]
+            arr = (ctypes.c_char_p * len(bufs))(*bufs)
+            lens = np.asarray([len(b) for b in bufs], dtype=np.int64)
+            nb = np.zeros((len(asc), cap), dtype=np.int32)
+            nc = np.zeros(len(asc), dtype=np.int32)
+            _native.call("mrag_hash_tokenize", ctypes.cast(arr, ctypes.c_void_p), lens.ctypes.data, len(asc),
+                         ids_of.lo, ids_of.hi, cap, min(8, decode_workers()), nb.ctypes.data, nc.ctypes.data)
+            sel = np.asarray(asc)
+            body[sel] = nb
+            counts[sel] = nc
+        except (OSError, ImportError):  # no library here: the Python path below
+            pass
+    for i in np.flatnonzero(counts < 0).tolist():
+        ids = ids_of(_basic_tokens(texts[i]))[:cap]
+        body[i, :len(ids)] = ids
+        counts[i] = len(ids)
+    return body, counts
+
+
+def _assemble(body: np.ndarray, counts: np.ndarray, first: int, last: int, pad: int) -> Tuple[np.ndarray, np.ndarray]:
+    """[first] + body[:count] + [last], padded with ``pad`` to the longest: (ids, mask) int32."""
+    n = len(counts)
+    T = int(counts.max()) + 2 if n else 2
+    col = np.arange(T, dtype=np.int32)[None, :]
+    c = counts.astype(np.int32)[:, None]
+    ids = np.full((n, T), pad, dtype=np.int32)
+    inner = (col >= 1) & (col <= c)
+    if T > 2:
+        ids[:, 1:T - 1] = np.where(inner[:, 1:T - 1], body[:, :T - 2], pad)
+    ids[:, 0] = first
+    ids[np.arange(n), counts + 1] = last
+    mask = (col < c + 2).astype(np.int32)
+    return ids, mask
+
+
 class WordPieceTokenizer:
     """MiniLM tokeniser: [CLS] ... [SEP], truncation to max_len (ST: 256)."""
 
@@ -83,6 +137,8 @@ class WordPieceTokenizer:
         return [self.CLS] + body[: self.max_len - 2] + [self.SEP]
 
     def __call__(self, texts: Sequence[str]) -> Tuple[np.ndarray, np.ndarray]:
+        if self._tok is None and len(texts) >= _NATIVE_MIN:
+            return _assemble(*_hash_bodies(texts, self._ids, self.max_len - 2), self.CLS, self.SEP, self.PAD)
         if self._tok is not None and len(texts) > 1:  # the fast tokeniser's batch form (its own threads)
             seqs = [e.ids for e in self._tok.encode_batch(list(texts))]
         else:
@@ -159,6 +215,10 @@ class ClipTokenizer:
         return [self.BOS] + self._ids(_basic_tokens(text)) + [self.EOS]
 
     def __call__(self, texts: Sequence[str]) -> Tuple[np.ndarray, np.ndarray]:
+        if self._tok is None and len(texts) >= _NATIVE_MIN:
+            body, counts = _hash_bodies(texts, self._ids, self.max_len - 1)
+            if int(counts.max()) < self.max_len - 1:  # else a text is too long: its exact length below
+                return _assemble(body, counts, self.BOS, self.EOS, self.EOS)
         seqs = [self.encode_one(t) for t in texts]
         T = max(len(s) for s in seqs)
         if T > self.max_len:
