@@ -35,6 +35,14 @@ for p in (PKG, ROOT):
 
 # synthetic encoder weights (random-init architecture; no hub checkpoints offline)
 os.environ.setdefault("MRAG_SYNTHETIC_WEIGHTS", "1")
+# HIP maps a process's streams onto GPU_MAX_HW_QUEUES hardware queues (HIP's default 4): with
+# the bench's in-flight legs (three CLIP batches, two kNN searches, four config-5 steps of two
+# branches, the image lanes' streams) two streams sharing a queue serialise. 8 queues, set before
+# the runtime starts (an explicit setting wins), as a serving process with that many concurrent
+# request streams would set it: CLIP three in flight 78k/86k (by which pool streams the leg got)
+# -> 87k, one batch 73.5-74.7k, config 5 257-261k; 16 queues cost config 5 ~8 %
+# (profiles/r6s26_r6s27_hw_queues.txt).
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
 
 ROWS_PER_GPU = 1 << 20
 DIM = 512
@@ -240,14 +248,31 @@ def _traffic_from_profiles():
         return None
 
 
-def clip_leg(steps: int, warmup: int):
+def _early_streams(dev, n: int):
+    """n HIP streams made (and each given one tiny kernel) before the bench's other legs create
+    and destroy theirs. HIP maps a process's streams onto GPU_MAX_HW_QUEUES hardware queues (4 by
+    default); streams taken late in the run from torch's pool landed two of the CLIP leg's three
+    on one queue for some pool positions (78k vs 86k img/s on one box,
+    profiles/r6s24_clip_stream_position.txt). A serving process makes its request streams once at
+    start-up, as these are."""
+    import torch
+
+    ss = [torch.cuda.Stream(device=dev) for _ in range(n)]
+    for s in ss:
+        with torch.cuda.stream(s):
+            torch.zeros(1, device=dev).add_(1)
+    torch.cuda.synchronize(dev)
+    return ss
+
+
+def clip_leg(steps: int, warmup: int, streams=None):
     """CLIP ViT-B/32 image embeds/s on one GPU (config 2: batch 256, fp16)."""
     try:
         from app.encoders import bench_clip_images
     except Exception:
         return None
-    out = bench_clip_images(steps=steps, warmup=warmup)  # three batches in flight
-    one = bench_clip_images(steps=steps, warmup=warmup, inflight=1)
+    out = bench_clip_images(steps=steps, warmup=warmup, streams=streams)  # three batches in flight
+    one = bench_clip_images(steps=steps, warmup=warmup, inflight=1, streams=streams)
     out["one_batch_in_flight"] = {"images_per_s": one["value"], "ms_per_batch": one["ms_per_batch"]}
     return out
 
@@ -1031,6 +1056,7 @@ def main():
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
     dev = torch.device("cuda", local)
+    clip_streams = _early_streams(dev, 3) if rank == 0 and not args.no_clip else None
 
     from app.vector_store import FlatIndex
 
@@ -1215,7 +1241,7 @@ def main():
                                        index_image_nodes=index_image, index_text_nodes=index_text_leg())
             call_pattern = out["call_pattern"]
         if not args.no_clip:
-            clip = clip_leg(steps=max(30, args.steps), warmup=3)  # single-GPU leg, rank 0; 30+ batches: three in flight reach steady state
+            clip = clip_leg(steps=max(30, args.steps), warmup=3, streams=clip_streams)  # single-GPU leg, rank 0; 30+ batches: three in flight reach steady state
             if clip is not None:
                 if not args.no_cpu_baseline:
                     clip["cpu_baseline"] = clip_cpu_baseline()

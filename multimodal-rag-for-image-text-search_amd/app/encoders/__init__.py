@@ -209,7 +209,7 @@ def load_encoder(cfg: EncoderConfig, model_name: Optional[str] = None, device: i
 
 
 def bench_clip_images(steps: int = 10, warmup: int = 2, batch: int = 256, device: int = 0,
-                      inflight: int = 3) -> Dict:
+                      inflight: int = 3, streams=None) -> Dict:
     """BASELINE config 2: CLIP ViT-B/32 image embeds/s on one GPU (batch 256 random
     224x224 u8 images resident in HBM, fp16 MFMA, synthetic weights).
 
@@ -220,13 +220,17 @@ def bench_clip_images(steps: int = 10, warmup: int = 2, batch: int = 256, device
     process with concurrent requests does (measured on one box: 1 -> 66.8k, 2 -> 66.8k,
     3 -> 81.9k, 4 -> 81.1k img/s; with two, the batches fall into step and their persistent
     GEMM grids queue behind each other). inflight=1 runs one batch at a time (on its own stream,
-    still without a host sync per batch)."""
+    still without a host sync per batch). ``streams``: the HIP streams to run on (a serving
+    process creates its request streams once at start-up; bench.py passes streams it made before
+    its other legs, so each lands on its own hardware queue, see bench.py _early_streams)."""
     import torch
 
     inflight = max(1, int(inflight))
     dev = torch.device("cuda", device)
     encs = [GpuEncoder(CLIP_VISION_B32, device=device) for _ in range(inflight)]
-    streams = [torch.cuda.Stream(device=dev) for _ in range(inflight)]
+    if streams is None or len(streams) < inflight:
+        streams = [torch.cuda.Stream(device=dev) for _ in range(inflight)]
+    streams = list(streams)[:inflight]
     g = torch.Generator(device=dev).manual_seed(2)
     imgs = torch.randint(0, 256, (batch, 224, 224, 3), generator=g, dtype=torch.uint8, device=dev)
     outs = [None] * inflight
