@@ -272,7 +272,10 @@ def clip_leg(steps: int, warmup: int, streams=None):
     except Exception:
         return None
     out = bench_clip_images(steps=steps, warmup=warmup, streams=streams)  # three batches in flight
-    one = bench_clip_images(steps=steps, warmup=warmup, inflight=1, streams=streams)
+    # one batch at a time on a stream from torch's pool, as before: its image lanes fork onto the
+    # handle's own lane stream, which shared a hardware queue with the start-up stream in three of
+    # four runs (53k instead of 74k img/s, profiles/r6s26_r6s27_hw_queues.txt)
+    one = bench_clip_images(steps=steps, warmup=warmup, inflight=1)
     out["one_batch_in_flight"] = {"images_per_s": one["value"], "ms_per_batch": one["ms_per_batch"]}
     return out
 
