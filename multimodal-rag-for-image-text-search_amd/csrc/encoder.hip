@@ -85,9 +85,11 @@ struct mrag_encoder {
   // workspace of a forward: w points at work[0], or at work[i] while image lane i is enqueued
   Work work[MRAG_IMG_LANES];
   Work* w = &work[0];
-  // image lanes 1.. (mrag_encoder_embed_images): their streams and the fork / join events
+  // image lanes (mrag_encoder_embed_images): their streams (every lane on one of the handle's
+  // own, made together), the fork event and one join event per lane
   hipStream_t lane_stream[MRAG_IMG_LANES] = {};
   hipEvent_t lane_ev[MRAG_IMG_LANES] = {};
+  hipEvent_t lane_fork = nullptr;
   // Device-pointer calls return without a host sync (stream-ordered, like any kernel launch):
   // `done` marks the end of the last call's work on `last_stream`; a call on another stream
   // first waits for it (the workspace is shared), and a workspace reallocation first
@@ -566,6 +568,7 @@ int mrag_encoder_destroy(mrag_encoder* e) {
       if (e->lane_stream[i]) (void)hipStreamDestroy(e->lane_stream[i]);
       if (e->lane_ev[i]) (void)hipEventDestroy(e->lane_ev[i]);
     }
+    if (e->lane_fork) (void)hipEventDestroy(e->lane_fork);
     (void)hipStreamDestroy(e->stream);
   }
   delete e;
@@ -716,11 +719,18 @@ int mrag_encoder_embed_images(mrag_encoder* e, const uint8_t* images, int32_t ba
   // batches in flight (profiles/r5s7_lanes_ab.jsonl). Every row depends only on its image (the
   // batch-consistency tests), so the result is bit-identical either way.
   int lanes = (MRAG_IMG_LANES > 1 && B >= MRAG_IMG_LANE_MIN && sole_image_handle(e)) ? MRAG_IMG_LANES : 1;
-  // the lanes' streams and events are created on first use: a handle that never runs alone holds
-  // no extra stream (streams share the process's hardware queues)
-  for (int i = 0; i < lanes && lanes > 1; ++i) {
-    if (i > 0 && !e->lane_stream[i]) MRAG_HIP(hipStreamCreateWithFlags(&e->lane_stream[i], hipStreamNonBlocking));
-    if (!e->lane_ev[i]) MRAG_HIP(hipEventCreateWithFlags(&e->lane_ev[i], hipEventDisableTiming));
+  // the lanes' streams and events are created on first use, all lanes' streams together: a
+  // handle that never runs alone holds no extra stream. Every lane runs on one of these, none on
+  // the caller's stream s: HIP puts the process's streams on GPU_MAX_HW_QUEUES hardware queues
+  // (4 by default), and a lane on s shared a queue with the other lane's stream whenever s had
+  // been made at another time (53k instead of 74k img/s one batch at a time,
+  // profiles/r6s26_r6s27_hw_queues.txt); streams made one after the other take different queues.
+  if (lanes > 1) {
+    for (int i = 0; i < lanes; ++i)
+      if (!e->lane_stream[i]) MRAG_HIP(hipStreamCreateWithFlags(&e->lane_stream[i], hipStreamNonBlocking));
+    for (int i = 0; i < lanes; ++i)
+      if (!e->lane_ev[i]) MRAG_HIP(hipEventCreateWithFlags(&e->lane_ev[i], hipEventDisableTiming));
+    if (!e->lane_fork) MRAG_HIP(hipEventCreateWithFlags(&e->lane_fork, hipEventDisableTiming));
   }
   struct ResetWork {  // e->w back to work[0] on every return
     mrag_encoder* e;
@@ -731,8 +741,8 @@ int mrag_encoder_embed_images(mrag_encoder* e, const uint8_t* images, int32_t ba
     int n;
     bool armed = true;
     ~DrainLanes() {
-      if (armed)
-        for (int i = 1; i < n; ++i) (void)hipStreamSynchronize(e->lane_stream[i]);
+      if (armed && n > 1)
+        for (int i = 0; i < n; ++i) (void)hipStreamSynchronize(e->lane_stream[i]);
     }
   } drain_lanes{e, lanes};
   e->w = &e->work[0];
@@ -747,19 +757,19 @@ int mrag_encoder_embed_images(mrag_encoder* e, const uint8_t* images, int32_t ba
     if (int rc = buf_ensure(e->w->OUT, (size_t)B * c.proj_dim * 4)) return rc;
     dst = (float*)e->w->OUT.p;
   }
-  if (lanes > 1) MRAG_HIP(hipEventRecord(e->lane_ev[0], s));  // fork
+  if (lanes > 1) MRAG_HIP(hipEventRecord(e->lane_fork, s));  // fork
   int b0 = 0;
   for (int i = 0; i < lanes; ++i) {
     const int nb = B / lanes + (i < B % lanes ? 1 : 0);
-    hipStream_t ls = i == 0 ? s : e->lane_stream[i];
-    if (i > 0) MRAG_HIP(hipStreamWaitEvent(ls, e->lane_ev[0], 0));
+    hipStream_t ls = lanes > 1 ? e->lane_stream[i] : s;
+    if (lanes > 1) MRAG_HIP(hipStreamWaitEvent(ls, e->lane_fork, 0));
     e->w = &e->work[i];
     if (int rc = ensure_workspace(e, nb, T)) return rc;
     if (int rc = image_forward(e, img + (size_t)b0 * S * S * 3, nb, dst + (size_t)b0 * c.proj_dim, normalize, ls))
       return rc;
     b0 += nb;
   }
-  for (int i = 1; i < lanes; ++i) {  // join
+  for (int i = 0; i < lanes && lanes > 1; ++i) {  // join
     MRAG_HIP(hipEventRecord(e->lane_ev[i], e->lane_stream[i]));
     MRAG_HIP(hipStreamWaitEvent(s, e->lane_ev[i], 0));
   }
