@@ -37,11 +37,11 @@ for p in (PKG, ROOT):
 os.environ.setdefault("MRAG_SYNTHETIC_WEIGHTS", "1")
 # HIP maps a process's streams onto GPU_MAX_HW_QUEUES hardware queues (HIP's default 4): with
 # the bench's in-flight legs (three CLIP batches, two kNN searches, four config-5 steps of two
-# branches, the image lanes' streams) two streams sharing a queue serialise. 8 queues, set before
-# the runtime starts (an explicit setting wins), as a serving process with that many concurrent
-# request streams would set it: CLIP three in flight 78k/86k (by which pool streams the leg got)
-# -> 87k, one batch 73.5-74.7k, config 5 257-261k; 16 queues cost config 5 ~8 %
-# (profiles/r6s26_r6s27_hw_queues.txt).
+# branches, the image lanes' streams) two streams sharing a queue serialise. 8 queues when the
+# environment does not say (set before the runtime starts); an explicit setting wins, and the GPU
+# pool's boxes export 4, so the driver's runs use 4 (the line records it as "hip_hw_queues").
+# With the CLIP leg's streams made at start-up and the image lanes on the handle's own streams
+# the legs measure alike at 4 and 8 (profiles/r6s26_r6s27_hw_queues.txt; 16 cost config 5 ~8 %).
 os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
 
 ROWS_PER_GPU = 1 << 20
@@ -1207,6 +1207,7 @@ def main():
             "vs_baseline": None,
             "dtype": "fp16 MFMA scan + f64 exact rescore",
             "data": "synthetic (N(0,1) rows L2-normalised, seeded; queries N(0,1))",
+            "hip_hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
             "config": {
                 "workload": "BASELINE config 3 (N=1) / config 4 (N>1): brute-force cosine top-10, 1M x 512 rows per GPU, 1000-query batch",
                 "rows_per_gpu": ROWS_PER_GPU,

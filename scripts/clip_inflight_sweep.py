@@ -1,9 +1,8 @@
-"""CLIP image tower batches in flight (2..6) with 8 hardware queues and streams made at start-up.
+"""CLIP image tower batches in flight (2..6) with every stream created up front.
 
-The round-4 sweep (1 -> 66.8k, 2 -> 66.8k, 3 -> 81.9k, 4 -> 81.1k img/s) ran with HIP's default
-4 hardware queues, where four request streams share queues with each other. This repeats it
-the way bench.py runs the leg now: GPU_MAX_HW_QUEUES=8 set before the runtime starts and every
-stream created up front. Rounds are interleaved; one JSON line per (round, inflight).
+Repeats the round-4 sweep (1 -> 66.8k, 2 -> 66.8k, 3 -> 81.9k, 4 -> 81.1k img/s) the way bench.py
+runs the leg now. GPU_MAX_HW_QUEUES=8 only when the environment does not set it (the GPU pool's
+boxes export 4). Rounds are interleaved; one JSON line per (round, inflight).
 
     python scripts/clip_inflight_sweep.py [--rounds 2] [--steps 30]
 """

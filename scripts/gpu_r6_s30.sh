@@ -1,5 +1,5 @@
 #!/bin/bash
-# Session 30: batches / steps in flight with 8 hardware queues (the round-4/5 sweeps ran with 4).
+# Session 30: batches / steps in flight (at the box's hardware-queue setting).
 # CLIP: 2..6 batches in flight, interleaved rounds; config 5: MRAG_FUSION_INFLIGHT 2 / 3 / 4 / 6
 # through bench.py (other legs off), interleaved rounds.
 set -o pipefail

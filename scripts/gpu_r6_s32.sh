@@ -1,5 +1,5 @@
 #!/bin/bash
-# Session 32: kNN searches in flight (--knn-streams 2 / 3 / 4) with 8 hardware queues, interleaved
+# Session 32: kNN searches in flight (--knn-streams 2 / 3 / 4) at the box's hardware-queue setting, interleaved
 # rounds, kNN leg only.
 set -o pipefail
 mkdir -p gpurun_out
