@@ -81,24 +81,28 @@ def _prepare_metadata(chunk: Chunk) -> Dict[str, Any]:
 
 
 _QUERY_POOL = None  # one worker thread: the CLIP-text query encode beside the MiniLM one
-_SIDE_STREAMS: Dict[int, Any] = {}
 
 
-def _image_query_on_side_stream(query: str, dev: int) -> np.ndarray:
+def _image_query_in_worker(query: str, dev: int) -> np.ndarray:
+    """The CLIP-text query encode on the worker thread with that thread's default stream current,
+    so the encoder runs it on its handle's own stream (made with the handle; a NULL stream
+    argument, include/mrag.h). A B = 1 encode is a chain of launch-bound kernels: what overlaps
+    with the caller's MiniLM encode and search is mostly the host side. Run inside a side stream
+    from torch's pool instead (the round-5 form) it measured slower and erratic: query pair
+    1.76-1.97 ms with 3.7 / 4.5 ms outliers against 1.59-1.72 ms this way
+    (`profiles/r6s33_r6s34_retrieve_stream_ab.jsonl`), the pool stream presumably sharing a HIP
+    hardware queue (4 per process on the GPU pool's boxes) with a stream the other encode used."""
     import torch
 
-    s = _SIDE_STREAMS.get(dev)
-    if s is None:
-        s = _SIDE_STREAMS.setdefault(dev, torch.cuda.Stream(device=dev))
-    with torch.cuda.device(dev), torch.cuda.stream(s):
+    with torch.cuda.device(dev):
         return embed_query_for_images(query)
 
 
 def _get_embeddings(query: str) -> Tuple[np.ndarray, np.ndarray]:
     """Both query vectors (reference :120-129: MiniLM, then CLIP text). On a GPU the two B = 1
-    encodes are independent chains of small kernels, so the CLIP-text one runs in a worker thread
-    on its own HIP stream while this thread runs MiniLM (the pair takes ~the longer of the two
-    instead of their sum; the vectors are the same, and an exception from either propagates)."""
+    encodes are independent chains of small launch-bound kernels, so the CLIP-text one runs in a
+    worker thread while this thread runs MiniLM (their host sides overlap; the vectors are the
+    same, and an exception from either propagates)."""
     text_vec, finish = _text_embedding_first(query)
     return text_vec, finish()
 
@@ -107,7 +111,7 @@ def _text_embedding_first(query: str):
     """``_get_embeddings`` in two halves: the MiniLM vector now, and ``finish()`` -> the CLIP-text
     vector, which also fills the query-embedding cache exactly as ``_get_embeddings`` does.
     retrieve_text runs its search and chunk lookup between the two (they need only the MiniLM
-    vector), while the CLIP-text encode is still running on its own stream."""
+    vector), while the CLIP-text encode is still running in the worker thread."""
     global _QUERY_POOL
     cached = get_query_embeddings(query)
     if cached:
@@ -120,7 +124,7 @@ def _text_embedding_first(query: str):
             from concurrent.futures import ThreadPoolExecutor
 
             _QUERY_POOL = ThreadPoolExecutor(max_workers=1, thread_name_prefix="mrag-query")
-        fut = _QUERY_POOL.submit(_image_query_on_side_stream, query, torch.cuda.current_device())
+        fut = _QUERY_POOL.submit(_image_query_in_worker, query, torch.cuda.current_device())
     try:
         text_vec = embed_text_batch([query])
     except BaseException:
@@ -160,7 +164,7 @@ def retrieve_text(user_id: str, query: str, top_k: Optional[int] = None) -> List
     if cached is not None:
         return cached
     # the search and the hits' chunks run while the CLIP-text query encode (needed only by
-    # retrieve_images) finishes on its own stream; both vectors are in the cache before this
+    # retrieve_images) finishes in the worker thread; both vectors are in the cache before this
     # returns or raises, as after the reference's _get_embeddings (an error of the CLIP-text
     # encode is the one raised, as there: it would have stopped the reference before the search)
     if _get_embeddings is _GET_EMBEDDINGS:

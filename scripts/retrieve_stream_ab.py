@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """The per-query retrieve leg (bench.retrieve_pattern_leg) with the CLIP-text query encode's
-stream varied, arms interleaved: "pool" = the package's side stream from torch's pool (as
-shipped), "prio" = a high-priority side stream, "same" = the worker thread encodes on the
-caller's current stream (host overlap only, the kernels of the two encodes serialise).
+stream varied, arms interleaved: "pool" = a side stream from torch's pool (the round-5
+form), "prio" = a high-priority side stream, "same" = the worker thread encodes on its current
+stream (host overlap only; the form shipped since session 34).
 GPU_MAX_HW_QUEUES comes from the environment (bench's import sets 8 unless it is set)."""
 import json
 import os
@@ -26,28 +26,25 @@ x = x / x.norm(dim=1, keepdim=True)
 ix = FlatIndex(bench.DIM)
 ix.add(x)
 del x
-own = rmod._image_query_on_side_stream
+own = rmod._image_query_in_worker
 pool_s = torch.cuda.Stream(device=dev)
 prio_s = torch.cuda.Stream(device=dev, priority=-1)
+side = {}
 
 
-def same_stream(query, d):
-    with torch.cuda.device(d):
+def on_side_stream(query, d):
+    with torch.cuda.device(d), torch.cuda.stream(side[0]):
         return rmod.embed_query_for_images(query)
 
 
 ARMS = ("pool", "prio", "same")
 for r in range(-1, rounds):  # round -1: every arm once, not reported (first-use costs)
     for arm in ARMS[r % 3:] + ARMS[:r % 3] if r >= 0 else ARMS:
-        rmod._SIDE_STREAMS.clear()
-        if arm == "pool":
-            rmod._SIDE_STREAMS[0] = pool_s
-            rmod._image_query_on_side_stream = own
-        elif arm == "prio":
-            rmod._SIDE_STREAMS[0] = prio_s
-            rmod._image_query_on_side_stream = own
+        if arm in ("pool", "prio"):
+            side[0] = pool_s if arm == "pool" else prio_s
+            rmod._image_query_in_worker = on_side_stream
         else:
-            rmod._image_query_on_side_stream = same_stream
+            rmod._image_query_in_worker = own
         clear_all_caches()
         out = bench.retrieve_pattern_leg(ix, reps=100)
         if r < 0:
@@ -55,4 +52,4 @@ for r in range(-1, rounds):  # round -1: every arm once, not reported (first-use
         print(json.dumps({"queues": os.environ.get("GPU_MAX_HW_QUEUES"), "arm": arm, "round": r,
                           "retrieve_text_ms": out["retrieve_text_ms"], "retrieve_images_ms": out["retrieve_images_ms"],
                           "query_pair_ms": out["query_pair_ms"]}), flush=True)
-rmod._image_query_on_side_stream = own
+rmod._image_query_in_worker = own
