@@ -819,9 +819,23 @@ __global__ __launch_bounds__(WS_THREADS) void gemm_ws_kernel(GemmArgs g, int P, 
     const int m = min(tile * WS_ROWS + row, g.M - 1);
     glds_x4(g.A + (size_t)m * g.lda + c * 8, lds_base + (uint32_t)(buf * TILE_BYTES + piece * 1024));
   };
-  // the first tile's pieces go out before the weight loads, so the two overlap
+  // the first tile's pieces go out first, then the bias, then the weights: the wait before the
+  // first tile (below) covers the pieces and the bias only, and each weight fragment is waited
+  // for at its first MFMA (the compiler counts the loads into AGPRs), so the weight panel lands
+  // under the first tile's MFMAs instead of before them
 #pragma unroll
   for (int i = 0; i < PW; ++i) stage_piece(0, r, i);
+  // branch-free (a branch here made the compiler wait for every load in flight at its join):
+  // without a bias the loads read the weights and the values are dropped
+  const bool has_bias = g.bias != nullptr;
+  float bias[NB][4];
+#pragma unroll
+  for (int cb = 0; cb < NB; ++cb) {
+    const float* bp = has_bias ? g.bias + n0 + 16 * cb + 4 * g4 : (const float*)g.W;
+    const f32x4 b4 = *(const f32x4*)bp;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) bias[cb][q] = has_bias ? b4[q] : 0.0f;
+  }
 
   // this wave's weight columns n0 + 16 cb + c16, all of K, in AGPRs for the launch
   half8 wf[KT][NB];
@@ -830,17 +844,6 @@ __global__ __launch_bounds__(WS_THREADS) void gemm_ws_kernel(GemmArgs g, int P, 
 #pragma unroll
     for (int cb = 0; cb < NB; ++cb)
       wf[kk][cb] = *(const half8*)(g.W + (size_t)(n0 + 16 * cb + c16) * g.ldw + 32 * kk + 8 * g4);
-#pragma unroll
-  for (int kk = 0; kk < KT; ++kk)
-#pragma unroll
-    for (int cb = 0; cb < NB; ++cb) asm volatile("" ::"a"(wf[kk][cb]));
-  float bias[NB][4];
-#pragma unroll
-  for (int cb = 0; cb < NB; ++cb) {
-    const f32x4 b4 = g.bias ? *(const f32x4*)(g.bias + n0 + 16 * cb + 4 * g4) : f32x4{};
-#pragma unroll
-    for (int q = 0; q < 4; ++q) bias[cb][q] = b4[q];
-  }
 
   // A fragment (kk, rb): row 16 rb + c16, chunk 4 kk + g4 -> position (4 kk + g4) ^ c16
   const int offA0 = c16 * ROW_BYTES + 16 * (g4 ^ c16);
@@ -939,11 +942,16 @@ __global__ __launch_bounds__(WS_THREADS) void gemm_ws_kernel(GemmArgs g, int P, 
     __syncthreads();
   };
 
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the first tile and the weights
+  // the first tile's pieces and the bias (issued before the KT NB weight loads; the field holds
+  // at most 63, which then also waits for the first weight loads)
+  vmcnt_wait_c<(KT * NB < 63 ? KT * NB : 63)>();
   __syncthreads();
-  for (int it = 0; it < my_tiles; it += 2) {
-    tile_body(std::integral_constant<int, 0>{}, it);
-    if (it + 1 < my_tiles) tile_body(std::integral_constant<int, 1>{}, it + 1);
+  // the first tile outside the loop: inside it the compiler waits for each weight fragment just
+  // before its first MFMA; a loop using them would have all of them waited for at its entry
+  tile_body(std::integral_constant<int, 0>{}, 0);
+  for (int it = 1; it < my_tiles; it += 2) {
+    tile_body(std::integral_constant<int, 1>{}, it);
+    if (it + 1 < my_tiles) tile_body(std::integral_constant<int, 0>{}, it + 1);
   }
   // the image holds the second-to-last tile's rows (written during the last tile): out with them
   if (my_tiles > 1) {
