@@ -1687,7 +1687,10 @@ int launch_ws(const GemmArgs& g, int epi, hipStream_t s) {
 
 int launch_gemm_ws(const GemmArgs& g, int epi, hipStream_t s) {
   MRAG_REQUIRE(gemm_ws_fits(g, epi), "gemm K3w: shape M=%d N=%d K=%d epilogue %d unsupported", g.M, g.N, g.K, epi);
-  const bool nb4 = g.N % 256 == 0;
+  // K = 384 takes NB = 3 wherever N allows it: MiniLM fc1 (N = 1536, both fit) 43.1-43.2 -> 39.5-40.9
+  // us alone, eight panels on all 256 CUs instead of six on 240; at K = 512 (CLIP-text q|k|v, also
+  // both) NB = 3 measured no faster (profiles/r6s38_k3w_nb3_ab.jsonl)
+  const bool nb4 = g.N % 256 == 0 && !(g.K == 384 && g.N % 192 == 0);
   if (g.K == 512) return nb4 ? launch_ws<4, 16>(g, epi, s) : launch_ws<3, 16>(g, epi, s);
   return nb4 ? launch_ws<4, 12>(g, epi, s) : launch_ws<3, 12>(g, epi, s);
 }
